@@ -1,0 +1,269 @@
+"""bench.py -- pod-node pair scores/s and placements/s of the MI355X placement
+engine on BASELINE.json's headline workload:
+
+  synthetic 10k nodes x 100k pending pods, dense int8 latency matrix and
+  pod->node traffic (rack/zone locality, 8 bound peers per pod), clusterloader2-
+  shaped requests -- all generated in HBM before the timed region.
+
+One step = one full placement pass: resource-fit filter over all pod x node
+pairs, the WA x L contraction on MFMA with the fused top-4 epilogue, the
+per-pod merge (+ RCCL all-gather across node shards when N > 1), and the
+greedy commit with capacity update; the placements and integer scores are
+copied back to the host.  The reference-mode vote scorer (scheduler.go:248-394
+on one fresh 10k-node snapshot per pod, 48 GB) is timed too and reported under
+"reference_mode".
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_I8_TOPS = 5033.2     # dense int8 MFMA, 256 CU x 4 SIMD x 2048 op/clk x 2.4 GHz
+PEAK_BF16_TFLOPS = 2516.6  # dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0      # HBM3E spec (MI355X_MICROARCH.md)
+SEED = 0x4E4153
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes", type=int, default=10000)
+    ap.add_argument("--pods", type=int, default=100000)
+    ap.add_argument("--dtype", default="i8", choices=["i8", "bf16"])
+    ap.add_argument("--peers", type=int, default=8)
+    ap.add_argument("--no-reference-mode", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--only", choices=["place", "vote"], default=None,
+                    help="profile helper: run only one path")
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self, gpus):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if self.world != gpus:
+            raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={self.world}")
+        self.pg = None
+        import torch
+        self.torch = torch
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.dist = dist
+        torch.cuda.set_device(self.local)
+
+    def barrier_sync(self):
+        self.torch.cuda.synchronize()
+        if self.world > 1:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def bcast_bytes(self, b):
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+
+def time_steps(d, fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    d.barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    d.barrier_sync()
+    return d.max(time.perf_counter() - t0)
+
+
+def bench_place(args, d, eng):
+    N, P = args.nodes, args.pods
+    if d.world > 1:
+        uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
+        eng.comm_init(uid, d.rank, d.world)
+    eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+    acc = {"cost_ms": 0.0, "fit_ms": 0.0, "merge_ms": 0.0, "commit_ms": 0.0, "total_ms": 0.0,
+           "cost_launches": 0, "rescore_rounds": 0, "unschedulable": 0}
+    state = {"n": 0, "node": None}
+
+    def step():
+        eng.reset_capacity()
+        node, _, score = eng.place(want_cost=True)
+        t = eng.timings()
+        if state["n"] >= 0:
+            for k in acc:
+                acc[k] += t[k]
+            state["n"] += 1
+        state["node"] = node
+
+    for _ in range(args.warmup):
+        step()
+    for k in acc:
+        acc[k] = 0
+    state["n"] = 0
+    elapsed = time_steps(d, step, args.steps, 0)
+    n = max(1, state["n"])
+    per = {k: v / n for k, v in acc.items()}
+    return elapsed, per, state["node"]
+
+
+def bench_vote(args, d, eng):
+    N = args.nodes
+    S = args.pods // d.world
+    eng.synth_snapshots(SEED + d.rank, N, S)
+    rng = np.random.default_rng(SEED)
+    o1 = rng.permutation(N).astype(np.int32)
+    o2 = rng.permutation(N + 1).astype(np.int32)
+    eng.upload_orders(o1, o2)
+    vote_ms = [0.0]
+
+    def step():
+        eng.score_reference(S)
+        vote_ms[0] += eng.timings()["vote_ms"]
+
+    for _ in range(args.warmup):
+        step()
+    vote_ms[0] = 0.0
+    elapsed = time_steps(d, step, args.steps, 0)
+    best, win = eng.score_reference(S)
+    return elapsed, vote_ms[0] / args.steps, S, (o1, o2, best, win)
+
+
+def cpu_baseline_place(args, eng, gpu_nodes):
+    """Oracle (C restatement, OpenMP) on a bounded sample of the same workload:
+    the first Ps pods against all N nodes.  Sequential greedy over pods 0..Ps-1
+    depends only on those pods, so the GPU's placements for them must match."""
+    import oracle
+    N = args.nodes
+    threads = min(16, os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    _, L, cap, req = eng.read_inputs(0, 0, want_L=True)
+    Ps, spent, t_total, pods_done = 64, 0.0, 0.0, 0
+    placements = None
+    while True:
+        WA, _, _, _ = eng.read_inputs(0, Ps, want_L=False)
+        t0 = time.perf_counter()
+        node, _, _ = oracle.place(WA, L, req[:Ps], cap, args.dtype)
+        dt = time.perf_counter() - t0
+        spent += dt
+        t_total, pods_done, placements = dt, Ps, node
+        if spent > args.cpu_budget_s / 3 or Ps >= 4096:
+            break
+        Ps *= 2
+    match = bool((gpu_nodes[:pods_done] == placements).all())
+    return {"value": pods_done * N / t_total, "unit": "pair-scores/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle/oracle.c or_place (sequential greedy, cost rows on {threads} "
+                      f"OpenMP threads) on the first {pods_done} pods x {N} nodes of the same "
+                      f"workload, {t_total:.2f} s",
+            "placements_per_s": pods_done / t_total,
+            "gpu_matches_oracle_on_sample": match}
+
+
+def cpu_baseline_vote(args, eng, ref):
+    """Literal restatement of scheduler.go:250-394 (single thread, the
+    reference's single Schedule goroutine) on sampled snapshots."""
+    import oracle
+    o1, o2, best, win = ref
+    N = args.nodes
+    snaps, idx = [], list(range(0, min(eng.snap_count, 4000), 7))
+    t_total, done, ok = 0.0, 0, True
+    for s in idx:
+        snap = eng.read_snapshot(s)
+        t0 = time.perf_counter()
+        b, w, _ = oracle.vote(snap, o1, o2)
+        t_total += time.perf_counter() - t0
+        done += 1
+        ok &= (b == best[s]) and (list(w) == win[s].tolist())
+        if t_total > args.cpu_budget_s / 6:
+            break
+    return {"value": done * N / t_total, "unit": "pair-scores/s", "cores": 1, "kind": "port",
+            "sample": f"oracle or_vote_literal (C restatement of scheduler.go:250-394, one "
+                      f"thread like wait.Until(Schedule)) on {done} sampled snapshots x {N} nodes",
+            "gpu_matches_oracle_on_sample": bool(ok)}
+
+
+def main():
+    args = parse()
+    d = Dist(args.gpus)
+    from kubernetesnetawarescheduler_amd import Engine
+    eng = Engine(d.local)
+    N, P = args.nodes, args.pods
+    out = {"metric": "pod-node pair scores/sec and placements/sec at 10k nodes x 100k pods",
+           "unit": "pair-scores/s", "n_gpus": d.world, "steps": args.steps,
+           "warmup": args.warmup, "higher_is_better": True, "scaling": "strong",
+           "vs_baseline": None, "dtype": "i8xi8->i32" if args.dtype == "i8" else "bf16xbf16->f32",
+           "data": "synthetic (seeded, generated in HBM)",
+           "config": {"workload": f"C3: {N} nodes x {P} pods, dense {args.dtype} latency + "
+                                  f"traffic, racks of 32 / zones of 16 racks, {args.peers} "
+                                  f"peers per pod, clusterloader2-shaped requests",
+                      "nodes": N, "pods": P, "parallelism": f"node-sharded x{d.world}",
+                      "candidates_per_pod": 4}}
+    gpu_nodes = None
+    if args.only != "vote":
+        elapsed, per, gpu_nodes = bench_place(args, d, eng)
+        ms = elapsed * 1e3 / args.steps
+        out["value"] = P * N / (elapsed / args.steps)
+        out["ms_per_step"] = ms
+        out["placements_per_s"] = P / (elapsed / args.steps)
+        nloc = N // d.world
+        ops = 2.0 * P * N * nloc * max(1, per["cost_launches"]) / max(1, per["cost_launches"])
+        cost_ms = per["cost_ms"] / max(1, per["cost_launches"])
+        achieved = ops / (cost_ms * 1e-3) / 1e12
+        peak = PEAK_I8_TOPS if args.dtype == "i8" else PEAK_BF16_TFLOPS
+        out["roofline"] = {"kernel": "k_cost_topk", "bound": "mfma", "achieved": achieved,
+                           "peak": peak, "unit": "TOPS" if args.dtype == "i8" else "TFLOP/s",
+                           "frac": achieved / peak, "traffic": None,
+                           "launch_ms": cost_ms, "ops_per_launch": ops}
+        out["stages_ms"] = {k: per[k] for k in ("fit_ms", "cost_ms", "merge_ms", "commit_ms",
+                                                "total_ms")}
+        out["rescore_rounds"] = per["rescore_rounds"]
+        out["unschedulable"] = per["unschedulable"]
+    if not args.no_reference_mode and args.only != "place":
+        elapsed, vote_ms, S, ref = bench_vote(args, d, eng)
+        bytes_launch = 48.0 * N * S
+        out["reference_mode"] = {
+            "value": S * d.world * N / (elapsed / args.steps), "unit": "pair-scores/s",
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "workload": f"vote scorer, one fresh {N}-node snapshot per pod ({S * d.world} pods)",
+            "roofline": {"kernel": "k_vote", "bound": "hbm",
+                         "achieved": bytes_launch / (vote_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s",
+                         "frac": bytes_launch / (vote_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                         "traffic": None, "launch_ms": vote_ms, "bytes_per_launch": bytes_launch}}
+        if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+            out["reference_mode"]["cpu_baseline"] = cpu_baseline_vote(args, eng, ref)
+    if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and gpu_nodes is not None:
+        # the vote path freed nothing; re-synthesise the cluster inputs (same seed)
+        eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+        out["cpu_baseline"] = cpu_baseline_place(args, eng, gpu_nodes)
+    eng.close()
+    if d.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+/*
+ * nas.h -- C ABI of the MI355X network-aware placement engine.
+ *
+ * Drop-in boundary for the placement decision of
+ * pablojara/kubernetesNetAwareScheduler (scheduler/scheduler.go):
+ *
+ *   func (s *CustomScheduler) findNodesThatFit(pod *v1.Pod) (string, error)   :239
+ *     -> prioritize(nodes, pod) map[string]int                                :248
+ *     -> findBestNode(priorities) string                                      :384
+ *
+ * The Go host (or the C++ host mirror in kubernetesnetawarescheduler_amd/host)
+ * keeps the node-name table, the informer loop and Bind; this library deals in
+ * node INDICES only.  INTEGRATION.md shows the cgo binding.
+ *
+ * Conventions
+ *  - Every entry returns int: NAS_OK (0) or a negative NAS_ERR_*; on error
+ *    nas_last_error(ctx) holds a message.  No C++ exception crosses the ABI.
+ *  - All pointers are HOST pointers owned by the caller and are not retained
+ *    after the call returns (cgo pointer rules).  Device memory is owned by
+ *    the context.  Every call is blocking: it synchronises the context's HIP
+ *    stream before returning, like the Go function it replaces.
+ *  - A context is NOT thread-safe (one per goroutine / OS thread); each entry
+ *    re-binds the context's HIP device, so a cgo call may land on any thread.
+ *  - Node codes in outputs: >= 0 node index, NAS_NONE (-2) the "none"
+ *    pseudo-node (scheduler.go:267-272, :364; Bind to it fails at :207),
+ *    NAS_EMPTY (-1) the empty string findBestNode returns when no score is
+ *    positive (:386) -- and, in extended mode, "no node fits".
+ */
+#ifndef NAS_H_
+#define NAS_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NAS_ABI_VERSION 1
+
+/* status codes */
+#define NAS_OK 0
+#define NAS_ERR_ARG (-1)         /* bad argument (null, size, not a permutation, ...) */
+#define NAS_ERR_HIP (-2)         /* HIP runtime error (also: no GPU / extension missing) */
+#define NAS_ERR_STATE (-3)       /* call out of order (e.g. nas_place before uploads) */
+#define NAS_ERR_NOMEM (-4)       /* device allocation failed */
+#define NAS_ERR_COMM (-5)        /* RCCL error */
+#define NAS_ERR_UNSUPPORTED (-6) /* size or dtype outside what the kernels support */
+
+/* node codes */
+#define NAS_NONE (-2)
+#define NAS_EMPTY (-1)
+
+/* element types of the traffic (WA) and latency (L) matrices */
+#define NAS_DT_I8 1   /* int8, int32 accumulation: exact integer scores */
+#define NAS_DT_BF16 2 /* bf16 bits (uint16), fp32 accumulation */
+
+/* winner slots returned by nas_score_reference (order of scheduler.go:360-365) */
+#define NAS_W_CPU 0
+#define NAS_W_MEM 1
+#define NAS_W_NETSENT 2
+#define NAS_W_NETREC 3
+#define NAS_W_BANDWIDTH 4 /* always NAS_NONE: the :353 bug */
+#define NAS_W_DISK 5
+
+/* number of candidates kept per pod between scoring and commit */
+#define NAS_K_CANDIDATES 4
+
+typedef struct nas_ctx nas_ctx;
+
+typedef struct nas_config {
+    int32_t device;   /* HIP device ordinal */
+    int32_t flags;    /* reserved, 0 */
+    int32_t reserved0;
+    int32_t reserved1;
+} nas_config;
+
+/* per-stage device times of the last nas_place / nas_score_reference call,
+ * measured with HIP events on the context's stream */
+typedef struct nas_timings {
+    float fit_ms;      /* resource-fit filter kernel */
+    float cost_ms;     /* MFMA contraction + fused top-k epilogue (all launches) */
+    float merge_ms;    /* per-pod merge of node-tile candidate lists (+ comm) */
+    float commit_ms;   /* greedy commit kernel(s) */
+    float vote_ms;     /* reference-mode vote kernel */
+    float total_ms;    /* whole call, device side */
+    int32_t cost_launches;   /* launches of the contraction kernel */
+    int32_t rescore_rounds;  /* commit stops that needed a rescore */
+    int32_t unschedulable;   /* pods with no fitting node */
+    int32_t reserved;
+} nas_timings;
+
+/* ---- lifecycle --------------------------------------------------------- */
+int nas_version(void);
+int nas_create(nas_ctx **out, const nas_config *cfg);
+void nas_destroy(nas_ctx *ctx);
+const char *nas_last_error(nas_ctx *ctx);
+int nas_get_timings(nas_ctx *ctx, nas_timings *out);
+
+/* ---- reference mode: the vote scorer of scheduler.go:248-394 ---------------
+ *
+ * Snapshot = one PrometheusNodeMetrics record per node (scheduler.go:24-32),
+ * SoA, n_snapshots blocks of n_nodes: field[s * n_nodes + node].  Go `int` is
+ * int64 (rx, tx, disk).  The reference scrapes a fresh snapshot per pod
+ * (:275-279); here pod p scores against snapshot pod_snapshot[p].
+ */
+int nas_upload_snapshot(nas_ctx *ctx, const double *cpu, const double *mem, const int64_t *rx,
+                        const int64_t *tx, const double *bw, const int64_t *disk,
+                        int32_t n_nodes, int32_t n_snapshots);
+
+/* Go map iteration orders, made explicit: order1[n_nodes] is the order of
+ * `range nodeMetricsMap` (:334); order2[n_nodes+1] the order of
+ * `range priorities` (:387), where value n_nodes is the "none" key.
+ * n_orders == 1: one order set for every snapshot; n_orders == n_snapshots:
+ * one per snapshot.  Both must be permutations (NAS_ERR_ARG otherwise). */
+int nas_upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
+                      int32_t n_orders);
+
+/* Score P pods.  order1/order2 non-NULL: one shared order set for this call;
+ * NULL: the sets from nas_upload_orders.  pod_snapshot NULL: pod p uses
+ * snapshot p.  best_out[P]: node index / NAS_NONE / NAS_EMPTY (the
+ * findNodesThatFit result, :245).  winners_out[P*6] optional (NAS_W_*). */
+int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
+                        const int32_t *pod_snapshot, int32_t P, int32_t *best_out,
+                        int32_t *winners_out);
+
+/* ---- extended mode: fit -> network cost -> top-k -> greedy commit ---------
+ *
+ * Resources are int32: cpu in millicores, memory in KiB, pod slots.
+ */
+
+/* Dense latency matrix L[m * n + j] = latency from node m to node j,
+ * uploaded once (dtype NAS_DT_I8 or NAS_DT_BF16). */
+int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n);
+
+/* Free capacity per node; also resets the working capacity nas_place uses. */
+int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *mem_kib,
+                        const int32_t *pods, int32_t n);
+
+/* Reset the working capacity to the last uploaded capacity. */
+int nas_reset_capacity(nas_ctx *ctx);
+
+/* Read back the working (remaining) capacity. */
+int nas_get_capacity(nas_ctx *ctx, int32_t *cpu_milli, int32_t *mem_kib, int32_t *pods,
+                     int32_t n);
+
+/* Pending pods in placement order: resource requests (>= 0). */
+int nas_upload_pods(nas_ctx *ctx, const int32_t *req_cpu_milli, const int32_t *req_mem_kib,
+                    const int32_t *req_pods, int32_t P);
+
+/* Traffic of each pending pod to each node, WA[p * n + m] = sum of
+ * W[p,q] over already-bound peers q with node(q) == m (dense, same dtype as L). */
+int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_t P, int32_t n);
+
+/* Same from a sparse pod-communication graph: for pod p the peers are
+ * peer_node[row_ptr[p] .. row_ptr[p+1]) (node of an already-bound peer, or
+ * -1 for an unbound peer, which is skipped) with weights weight[...]
+ * (int8 for NAS_DT_I8 -- summed in int32, saturated to [-128, 127] -- or bf16
+ * bits for NAS_DT_BF16, summed in fp32 and rounded once).  Aggregated on the
+ * device into the dense WA. */
+int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *peer_node,
+                           const void *weight, int32_t dtype, int32_t P, int32_t n,
+                           int64_t nnz);
+
+/* Resource-fit filter over all pod x node pairs against the working capacity.
+ * mask_out (optional) receives ceil(n/64) * P uint64 words, node-chunk major:
+ * bit j of mask_out[c * P + p] == pod p fits node 64c + j. */
+int nas_filter(nas_ctx *ctx, uint64_t *mask_out);
+
+/* Place all uploaded pods: fit, cost = WA x L on MFMA with the top-k fused
+ * in the epilogue, then greedy commit in pod order with capacity update.
+ * node_out[P]: chosen node or NAS_EMPTY.  cost_out[P] (optional): the
+ * chosen node's cost as float.  int_score_out[P] (optional): the chosen
+ * node's exact integer cost (NAS_DT_I8; 0 for bf16 or NAS_EMPTY). */
+int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_score_out);
+
+/* Scoring pass only (fit + cost/top-k + merge, no commit) against the
+ * working capacity; its lists are then read with nas_get_candidates. */
+int nas_score(nas_ctx *ctx);
+
+/* Candidate lists of the last scoring pass (nas_score, or nas_place after
+ * its rescore rounds): cand_node[P*K] (sorted by (cost, node); -1 past
+ * count), cand_cost_i[P*K] exact int cost (NAS_DT_I8), cand_cost_f[P*K]
+ * cost as float, count[P].  Any output may be NULL. */
+int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i,
+                       float *cand_cost_f, int32_t *count);
+
+/* ---- multi-GPU: node axis sharded over the GPUs of one node ---------------
+ * Rank r of `world` owns node columns [r*n/world, (r+1)*n/world) of L; pods,
+ * WA and capacities are replicated.  Per-pod candidate lists are exchanged
+ * with an RCCL all-gather over xGMI and merged; the commit is replicated, so
+ * every rank returns the same placements. */
+int nas_comm_unique_id(uint8_t id_out[128]);
+int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world);
+
+/* ---- synthetic inputs generated in HBM (benchmarks; seeded, deterministic) */
+/* Reference-mode snapshots per SURVEY.md §8(d) C1/C3. */
+int nas_synth_snapshots(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t n_snapshots);
+/* Read back snapshot s (to check sampled pods against a CPU oracle). */
+int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t *rx,
+                      int64_t *tx, double *bw, int64_t *disk);
+/* Extended-mode cluster: racks of 32 nodes in zones of 16 racks; latency by
+ * distance class; each pod has `peers` bound peers in one rack, traffic
+ * concentrated there; capacity and requests per SURVEY.md §8(d) C2/C3. */
+int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, int32_t dtype,
+                      int32_t peers);
+/* Read back rows of the device-resident inputs (for sampled oracle checks):
+ * WA rows [p0, p0+np), the full L, capacity and requests. */
+int nas_read_inputs(nas_ctx *ctx, int32_t p0, int32_t np, void *WA_rows, void *L,
+                    int32_t *cap_cpu, int32_t *cap_mem, int32_t *cap_pods, int32_t *req_cpu,
+                    int32_t *req_mem, int32_t *req_pods);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NAS_H_ */

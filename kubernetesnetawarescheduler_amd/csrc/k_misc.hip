@@ -1,0 +1,309 @@
+// k_misc.hip -- layout kernels (latency transpose, sparse traffic
+// aggregation) and seeded synthetic input generators that write straight
+// into HBM (benchmarks; SURVEY.md §8(d) workload shapes).
+#include "nas_internal.h"
+
+namespace nas {
+namespace {
+
+// ---------------------------------------------------------------- transpose
+// Lt[i][m] = L[m][n0 + i] for i < nloc, m < N; zero padding up to Mp x Kp.
+template <typename T>
+__global__ void k_transpose(const T *__restrict__ L, int N, int n0, int nloc, int Mp, int Kp,
+                            T *__restrict__ Lt) {
+    __shared__ T tile[64][65];
+    const int m0 = blockIdx.x * 64;  // source row block (contraction index m)
+    const int i0 = blockIdx.y * 64;  // destination row block (local node i)
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+    for (int r = ty; r < 64; r += 4) {
+        const int m = m0 + r, i = i0 + tx;
+        tile[r][tx] = (m < N && i < nloc) ? L[(size_t)m * N + n0 + i] : T(0);
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int i = i0 + r, m = m0 + tx;
+        if (i < Mp && m < Kp) Lt[(size_t)i * Kp + m] = tile[tx][r];
+    }
+}
+
+// --------------------------------------------------------- CSR aggregation
+// WA[p][m] = sum of weights of p's peers bound to node m (row zeroed before).
+// One thread per pod; peers per pod are few, so the O(nnz_p^2) dedupe walk is
+// cheap and needs no atomics.
+__global__ void k_csr_i8(const int *__restrict__ row_ptr, const int *__restrict__ peer,
+                         const signed char *__restrict__ w, int P, int N, int Kp,
+                         signed char *__restrict__ WA) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const int b = row_ptr[p], e = row_ptr[p + 1];
+    for (int x = b; x < e; ++x) {
+        const int m = peer[x];
+        if (m < 0 || m >= N) continue;
+        bool seen = false;
+        for (int y = b; y < x && !seen; ++y) seen = peer[y] == m;
+        if (seen) continue;
+        int s = 0;
+        for (int y = x; y < e; ++y) s += peer[y] == m ? (int)w[y] : 0;
+        WA[(size_t)p * Kp + m] = (signed char)max(-128, min(127, s));
+    }
+}
+
+__global__ void k_csr_bf16(const int *__restrict__ row_ptr, const int *__restrict__ peer,
+                           const unsigned short *__restrict__ w, int P, int N, int Kp,
+                           unsigned short *__restrict__ WA) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    const int b = row_ptr[p], e = row_ptr[p + 1];
+    for (int x = b; x < e; ++x) {
+        const int m = peer[x];
+        if (m < 0 || m >= N) continue;
+        bool seen = false;
+        for (int y = b; y < x && !seen; ++y) seen = peer[y] == m;
+        if (seen) continue;
+        float s = 0.f;
+        for (int y = x; y < e; ++y)
+            if (peer[y] == m) s += __uint_as_float((unsigned)w[y] << 16);
+        // round to nearest even bf16 (s is finite)
+        const unsigned u = __float_as_uint(s);
+        WA[(size_t)p * Kp + m] = (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+    }
+}
+
+// ---------------------------------------------------------------- synthetic
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ unsigned long long hsh(unsigned long long seed, unsigned long long a,
+                                                  unsigned long long b, unsigned long long c) {
+    return mix64(seed ^ mix64(a * 0x9e3779b97f4a7c15ull ^ mix64(b + 0x632be59bd9b4e019ull) ^
+                              (c << 48)));
+}
+__device__ __forceinline__ double unit(unsigned long long h) {  // [0, 1)
+    return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// Reference-mode snapshots, SURVEY.md §8(d) C1: cpu = mean of 4 per-core
+// frequencies in {0.6, 1.2, 1.5, 1.8} GHz (float32-rounded like
+// strconv.ParseFloat(s, 32), scheduler.go:423-441); mem% = 100 - avail*100/total
+// (:444-460) on float32-rounded byte counts; rx/tx ~ U[0, 1e6) with 10% zeros
+// (Atoi failures, :474-478); bw 0 for node 0 ("ubuntu", :287) and 20% of the
+// rest, else U(8e7, 9.5e7) bit/s; disk 0 in 30%, else U[1, 1000].
+__global__ void k_synth_snap(unsigned long long seed, int n, long long ns, int S,
+                             double *__restrict__ cpu, double *__restrict__ mem,
+                             double *__restrict__ bw, long long *__restrict__ rx,
+                             long long *__restrict__ tx, long long *__restrict__ disk) {
+    const long long total = (long long)S * ns;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const long long s = t / ns;
+        const int node = (int)(t - s * ns);
+        if (node >= n) {  // padding: never wins any comparison
+            cpu[t] = __longlong_as_double(0x7ff8000000000000ll);
+            mem[t] = cpu[t];
+            bw[t] = cpu[t];
+            rx[t] = 0x7fffffffffffffffll;
+            tx[t] = rx[t];
+            disk[t] = 0;
+            continue;
+        }
+        const unsigned long long h0 = hsh(seed, s, node, 1), h1 = hsh(seed, s, node, 2);
+        const unsigned long long h2 = hsh(seed, s, node, 3);
+        const float freqs[4] = {6e8f, 1.2e9f, 1.5e9f, 1.8e9f};
+        double f = 0;
+        for (int c = 0; c < 4; ++c) f += (double)freqs[(h0 >> (8 * c)) & 3];
+        cpu[t] = f / 4;
+        const float totalb = (float)(1073741824.0 * (1 + ((h0 >> 40) & 7)));
+        const float avail = (float)(unit(h1) * (double)totalb);
+        mem[t] = 100.0 - (((double)avail * 100.0) / (double)totalb);
+        rx[t] = ((h2 & 1023) < 102) ? 0 : (long long)((h2 >> 10) % 1000000);
+        tx[t] = (((h2 >> 30) & 1023) < 102) ? 0 : (long long)((h2 >> 40) % 1000000);
+        const unsigned long long h3 = hsh(seed, s, node, 4);
+        bw[t] = (node == 0 || (h3 & 1023) < 205) ? 0.0 : 8e7 + unit(h3 * 0x2545f4914f6cdd1dull) * 1.5e7;
+        disk[t] = ((h3 >> 12) % 100 < 30) ? 0 : (long long)(1 + (h3 >> 20) % 1000);
+    }
+}
+
+// Extended-mode cluster (build-defined):
+// nodes in racks of 32, racks in zones of 16; symmetric latency by distance
+// class (0 self, 2-4 same rack, 12-19 same zone, 40-105 cross zone);
+// capacity cpu {4000, 8000} m, memory {4, 8} GiB, 110 pods; requests
+// log-uniform over the clusterloader2 ranges (cpu 0.000213-0.5376 cores, mem
+// 7.6-311 MB, datasets/clusterloader2/*/*.json), 1 pod slot.
+__device__ __forceinline__ int lat(unsigned long long seed, int a, int b) {
+    if (a == b) return 0;
+    const int lo = min(a, b), hi = max(a, b);
+    const unsigned long long h = hsh(seed, lo, hi, 7);
+    if ((lo >> 5) == (hi >> 5)) return 2 + (int)(h % 3);
+    if ((lo >> 9) == (hi >> 9)) return 12 + (int)(h % 8);
+    return 40 + (int)((((hi >> 9) - (lo >> 9)) * 7) % 50) + (int)(h % 16);
+}
+
+template <typename T>
+__device__ __forceinline__ T from_int(int v);
+template <>
+__device__ __forceinline__ signed char from_int<signed char>(int v) { return (signed char)v; }
+template <>
+__device__ __forceinline__ unsigned short from_int<unsigned short>(int v) {
+    return (unsigned short)(__float_as_uint((float)v) >> 16);  // exact for |v| <= 256
+}
+
+template <typename T>
+__global__ void k_synth_lt(unsigned long long seed, int N, int n0, int nloc, int Mp, int Kp,
+                           T *__restrict__ Lt) {
+    const long long total = (long long)Mp * Kp;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int i = (int)(t / Kp), m = (int)(t - (long long)i * Kp);
+        Lt[t] = (i < nloc && m < N) ? from_int<T>(lat(seed, m, n0 + i)) : T(0);
+    }
+}
+
+template <typename T>
+__global__ void k_synth_lfull(unsigned long long seed, int N, T *__restrict__ L) {
+    const long long total = (long long)N * N;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int m = (int)(t / N), n = (int)(t - (long long)m * N);
+        L[t] = from_int<T>(lat(seed, m, n));
+    }
+}
+
+// one thread per pod: peers in the home rack (all but 2) and in the zone
+template <typename T>
+__global__ void k_synth_pods(unsigned long long seed, int N, int P, int peers, int Kp, int Pp,
+                             T *__restrict__ WA, int *__restrict__ req) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= Pp) return;
+    if (p >= P) { req[p] = 0; req[Pp + p] = 0; req[2 * Pp + p] = 0; return; }
+    const int n_racks = (N + 31) / 32;
+    const unsigned long long hp = hsh(seed, p, 0, 11);
+    const int rack = (int)(hp % n_racks);
+    int nodes[16], wts[16];
+    const int np = min(peers, 16);
+    for (int j = 0; j < np; ++j) {
+        const unsigned long long h = hsh(seed, p, j + 1, 12);
+        int node;
+        if (j < np - 2 || np <= 2) {
+            node = rack * 32 + (int)(h % 32);
+        } else {  // another rack of the same zone
+            const int zone0 = (rack >> 4) << 4;
+            const int r2 = min(zone0 + (int)((h >> 20) % 16), n_racks - 1);
+            node = r2 * 32 + (int)(h % 32);
+        }
+        nodes[j] = min(node, N - 1);
+        wts[j] = 16 + (int)((h >> 40) % 112);
+    }
+    for (int j = 0; j < np; ++j) {
+        bool seen = false;
+        for (int y = 0; y < j; ++y) seen |= nodes[y] == nodes[j];
+        if (seen) continue;
+        int s = 0;
+        for (int y = j; y < np; ++y) s += nodes[y] == nodes[j] ? wts[y] : 0;
+        WA[(size_t)p * Kp + nodes[j]] = from_int<T>(min(s, 127));
+    }
+    const unsigned long long hr = hsh(seed, p, 0, 13);
+    const double lc0 = -3.6716, lc1 = -0.2695;  // log10 of 0.000213, 0.5376 cores
+    const double lm0 = 6.8833, lm1 = 8.4928;    // log10 of 7.64e6, 3.11e8 bytes
+    const double cores = pow(10.0, lc0 + (lc1 - lc0) * unit(hr));
+    const double bytes = pow(10.0, lm0 + (lm1 - lm0) * unit(mix64(hr)));
+    req[p] = max(1, (int)ceil(cores * 1000.0));
+    req[Pp + p] = (int)ceil(bytes / 1024.0);
+    req[2 * Pp + p] = 1;
+}
+
+__global__ void k_synth_cap(unsigned long long seed, int N, int *__restrict__ cap) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= N) return;
+    const unsigned long long h = hsh(seed, n, 0, 21);
+    cap[n] = (h & 1) ? 8000 : 4000;
+    cap[N + n] = ((h >> 1) & 1) ? 8 * 1048576 : 4 * 1048576;
+    cap[2 * N + n] = 110;
+}
+
+inline int grid_for(long long total, int threads) {
+    long long g = (total + threads - 1) / threads;
+    return (int)(g < 65536 ? (g > 0 ? g : 1) : 65536);
+}
+
+}  // namespace
+
+hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
+                              int nloc, int Mp, int Kp, void *Lt) {
+    dim3 grid((Kp + 63) / 64, (Mp + 63) / 64);
+    if (dtype == NAS_DT_I8)
+        k_transpose<signed char><<<grid, 256, 0, st>>>(static_cast<const signed char *>(L_dev), N,
+                                                       n0, nloc, Mp, Kp,
+                                                       static_cast<signed char *>(Lt));
+    else
+        k_transpose<unsigned short><<<grid, 256, 0, st>>>(
+            static_cast<const unsigned short *>(L_dev), N, n0, nloc, Mp, Kp,
+            static_cast<unsigned short *>(Lt));
+    return hipGetLastError();
+}
+
+hipError_t launch_csr_aggregate(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
+                                const void *w, int dtype, int P, int N, int Kp, void *WA) {
+    if (P <= 0) return hipSuccess;
+    if (dtype == NAS_DT_I8)
+        k_csr_i8<<<(P + 255) / 256, 256, 0, st>>>(row_ptr, peer, static_cast<const signed char *>(w),
+                                                  P, N, Kp, static_cast<signed char *>(WA));
+    else
+        k_csr_bf16<<<(P + 255) / 256, 256, 0, st>>>(row_ptr, peer,
+                                                    static_cast<const unsigned short *>(w), P, N,
+                                                    Kp, static_cast<unsigned short *>(WA));
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int64_t ns, int S,
+                                  double *cpu, double *mem, double *bw, int64_t *rx, int64_t *tx,
+                                  int64_t *disk) {
+    k_synth_snap<<<grid_for((long long)S * ns, 256), 256, 0, st>>>(
+        seed, n, ns, S, cpu, mem, bw, reinterpret_cast<long long *>(rx),
+        reinterpret_cast<long long *>(tx), reinterpret_cast<long long *>(disk));
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
+                                int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
+                                int32_t *cap, int32_t *req, void *L_full) {
+    const size_t esz = dtype == NAS_DT_I8 ? 1 : 2;
+    hipError_t e;
+    if (Lt) {
+        if (dtype == NAS_DT_I8)
+            k_synth_lt<signed char><<<grid_for((long long)Mp * Kp, 256), 256, 0, st>>>(
+                seed, N, n0, nloc, Mp, Kp, static_cast<signed char *>(Lt));
+        else
+            k_synth_lt<unsigned short><<<grid_for((long long)Mp * Kp, 256), 256, 0, st>>>(
+                seed, N, n0, nloc, Mp, Kp, static_cast<unsigned short *>(Lt));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (L_full) {
+        if (dtype == NAS_DT_I8)
+            k_synth_lfull<signed char><<<grid_for((long long)N * N, 256), 256, 0, st>>>(
+                seed, N, static_cast<signed char *>(L_full));
+        else
+            k_synth_lfull<unsigned short><<<grid_for((long long)N * N, 256), 256, 0, st>>>(
+                seed, N, static_cast<unsigned short *>(L_full));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (WA) {
+        if ((e = hipMemsetAsync(WA, 0, (size_t)Pp * Kp * esz, st)) != hipSuccess) return e;
+        if (dtype == NAS_DT_I8)
+            k_synth_pods<signed char><<<(Pp + 255) / 256, 256, 0, st>>>(
+                seed, N, P, peers, Kp, Pp, static_cast<signed char *>(WA), req);
+        else
+            k_synth_pods<unsigned short><<<(Pp + 255) / 256, 256, 0, st>>>(
+                seed, N, P, peers, Kp, Pp, static_cast<unsigned short *>(WA), req);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (cap) {
+        k_synth_cap<<<(N + 255) / 256, 256, 0, st>>>(seed, N, cap);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace nas

@@ -1,0 +1,803 @@
+// nas_api.hip -- C ABI (include/nas.h) of the MI355X placement engine:
+// context, uploads into the HBM layouts of DESIGN.md, and the orchestration
+// of fit -> cost/top-k -> merge -> (RCCL exchange) -> commit with the rescore
+// loop.  Every entry re-binds the context's device and synchronises its
+// stream before returning (blocking semantics of the Go call it replaces).
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "nas_internal.h"
+
+using nas::DevBuf;
+using nas::KC;
+
+namespace nas {
+
+int fail(nas_ctx *ctx, int code, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int hip_fail(nas_ctx *ctx, hipError_t e, const char *what) {
+    return fail(ctx, NAS_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.p && b.bytes >= bytes) return NAS_OK;
+    if (b.p) {
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        b.bytes = 0;
+    }
+    hipError_t e = hipMalloc(&b.p, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        b.p = nullptr;
+        return fail(ctx, NAS_ERR_NOMEM,
+                    "hipMalloc(" + std::to_string(bytes) + "): " + hipGetErrorString(e));
+    }
+    b.bytes = bytes;
+    return NAS_OK;
+}
+
+}  // namespace nas
+
+#define HIPCK(expr)                                                  \
+    do {                                                             \
+        hipError_t e_ = (expr);                                      \
+        if (e_ != hipSuccess) return nas::hip_fail(ctx, e_, #expr);  \
+    } while (0)
+#define OK(expr)                   \
+    do {                           \
+        int r_ = (expr);           \
+        if (r_ != NAS_OK) return r_; \
+    } while (0)
+
+namespace {
+
+constexpr int RESCORE_PODS = 4096;  // pods rescored per commit stop (multiple of COST_BN)
+
+int bind(nas_ctx *ctx) {
+    if (!ctx) return NAS_ERR_ARG;
+    ctx->err.clear();
+    HIPCK(hipSetDevice(ctx->device));
+    return NAS_OK;
+}
+
+size_t esz(int dtype) { return dtype == NAS_DT_I8 ? 1 : 2; }
+
+int64_t kpad(int n, int dtype) { return nas::round_up(n, dtype == NAS_DT_I8 ? 128 : 64); }
+
+// event pool for per-stage device timing on the context stream
+struct Timer {
+    nas_ctx *ctx;
+    std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> spans;
+    static std::vector<hipEvent_t> &pool(nas_ctx *) {
+        static thread_local std::vector<hipEvent_t> p;
+        return p;
+    }
+    size_t used = 0;
+    std::vector<hipEvent_t> evs;
+    explicit Timer(nas_ctx *c) : ctx(c) {}
+    ~Timer() {
+        for (auto e : evs) (void)hipEventDestroy(e);
+    }
+    hipEvent_t ev() {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        evs.push_back(e);
+        return e;
+    }
+    hipEvent_t mark() {
+        hipEvent_t e = ev();
+        if (e) (void)hipEventRecord(e, ctx->stream);
+        return e;
+    }
+    void span(int which, hipEvent_t a, hipEvent_t b) { spans.push_back({which, {a, b}}); }
+    float total(int which) {
+        float s = 0;
+        for (auto &x : spans) {
+            if (x.first != which || !x.second.first || !x.second.second) continue;
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, x.second.first, x.second.second) == hipSuccess) s += ms;
+        }
+        return s;
+    }
+};
+enum { T_FIT, T_COST, T_MERGE, T_COMMIT, T_VOTE, T_TOTAL };
+
+int validate_perm(const int32_t *o, int n, std::vector<int32_t> &pos) {
+    pos.assign(n, -1);
+    for (int i = 0; i < n; ++i) {
+        if (o[i] < 0 || o[i] >= n || pos[o[i]] != -1) return -1;
+        pos[o[i]] = i;
+    }
+    return 0;
+}
+
+int upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, int32_t n_orders) {
+    const int n = ctx->snap_n;
+    if (n <= 0) return nas::fail(ctx, NAS_ERR_STATE, "upload a snapshot before its orders");
+    if (!order1 || !order2 || n_orders <= 0) return nas::fail(ctx, NAS_ERR_ARG, "orders");
+    const int64_t ns = nas::round_up(n, 2), ns2 = ns + 2;
+    std::vector<int32_t> o1((size_t)n_orders * ns, 0), p1((size_t)n_orders * ns, 0);
+    std::vector<int32_t> o2((size_t)n_orders * ns2, 0), p2((size_t)n_orders * ns2, 0);
+    std::vector<int32_t> pos;
+    for (int o = 0; o < n_orders; ++o) {
+        const int32_t *a = order1 + (size_t)o * n;
+        if (validate_perm(a, n, pos))
+            return nas::fail(ctx, NAS_ERR_ARG, "order1 set " + std::to_string(o) + " is not a permutation");
+        std::copy(a, a + n, o1.begin() + (size_t)o * ns);
+        std::copy(pos.begin(), pos.end(), p1.begin() + (size_t)o * ns);
+        const int32_t *b = order2 + (size_t)o * (n + 1);
+        if (validate_perm(b, n + 1, pos))
+            return nas::fail(ctx, NAS_ERR_ARG, "order2 set " + std::to_string(o) + " is not a permutation");
+        std::copy(b, b + n + 1, o2.begin() + (size_t)o * ns2);
+        std::copy(pos.begin(), pos.end(), p2.begin() + (size_t)o * ns2);
+    }
+    OK(nas::ensure(ctx, ctx->order1, o1.size() * 4));
+    OK(nas::ensure(ctx, ctx->pos1, p1.size() * 4));
+    OK(nas::ensure(ctx, ctx->order2, o2.size() * 4));
+    OK(nas::ensure(ctx, ctx->pos2, p2.size() * 4));
+    HIPCK(hipMemcpyAsync(ctx->order1.p, o1.data(), o1.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->pos1.p, p1.data(), p1.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->order2.p, o2.data(), o2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->pos2.p, p2.data(), p2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));  // host vectors die here
+    ctx->n_orders = n_orders;
+    ctx->ord_ns = ns;
+    return NAS_OK;
+}
+
+// shard geometry of the extended mode for n nodes / dtype
+void set_geometry(nas_ctx *ctx, int n, int dtype) {
+    ctx->N = n;
+    ctx->dtype = dtype;
+    ctx->Kp = (int32_t)kpad(n, dtype);
+    const int64_t a = (int64_t)ctx->rank * n / ctx->world;
+    const int64_t b = (int64_t)(ctx->rank + 1) * n / ctx->world;
+    ctx->Nloc0 = (int32_t)a;
+    ctx->Nloc = (int32_t)(b - a);
+    ctx->Mp = (int32_t)nas::round_up(std::max<int64_t>(ctx->Nloc, 1), nas::COST_BM);
+}
+
+int check_extended(nas_ctx *ctx) {
+    if (!ctx->have_L || !ctx->have_cap || !ctx->have_pods || !ctx->have_wa)
+        return nas::fail(ctx, NAS_ERR_STATE,
+                         "nas_place needs latency, capacity, pods and traffic uploaded");
+    return NAS_OK;
+}
+
+// scoring for pods [p_lo, p_hi): fit -> cost/top-k -> merge (-> exchange)
+int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi) {
+    hipStream_t st = ctx->stream;
+    const int pr0 = p_lo / nas::COST_BN * nas::COST_BN;
+    const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
+    const int np = pr1 - pr0;
+    auto *mask = ctx->mask.as<uint64_t>();
+    hipEvent_t e0 = tm.mark();
+    HIPCK(nas::launch_fit(st, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
+                          ctx->req.as<int32_t>(), ctx->P, ctx->Pp, p_lo, p_hi - p_lo, mask));
+    hipEvent_t e1 = tm.mark();
+    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, ctx->Pp,
+                                pr0, np, mask, ctx->partial.as<uint64_t>(), ctx->Nloc0));
+    hipEvent_t e2 = tm.mark();
+    const int n_lists = ctx->Mp / nas::COST_BM;
+    HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), n_lists, (int64_t)ctx->Pp * KC, 0,
+                            p_lo, p_hi - p_lo, ctx->cand_key.as<uint64_t>()));
+    if (ctx->world > 1) {
+        // exchange the per-shard top-4 of pods [pr0, pr1) and merge across ranks
+        const size_t cnt = (size_t)np * KC;
+        ncclResult_t r = ncclAllGather(ctx->cand_key.as<uint64_t>() + (size_t)pr0 * KC,
+                                       ctx->gather.as<uint64_t>(), cnt, ncclUint64,
+                                       reinterpret_cast<ncclComm_t>(ctx->comm), st);
+        if (r != ncclSuccess)
+            return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        HIPCK(nas::launch_merge(st, ctx->gather.as<uint64_t>(), ctx->world, (int64_t)cnt, pr0,
+                                p_lo, p_hi - p_lo, ctx->cand_key.as<uint64_t>()));
+    }
+    hipEvent_t e3 = tm.mark();
+    tm.span(T_FIT, e0, e1);
+    tm.span(T_COST, e1, e2);
+    tm.span(T_MERGE, e2, e3);
+    ctx->timings.cost_launches += 1;
+    return NAS_OK;
+}
+
+int alloc_extended(nas_ctx *ctx) {
+    const size_t chunks = ctx->Mp / 64;
+    OK(nas::ensure(ctx, ctx->mask, chunks * ctx->Pp * 8));
+    OK(nas::ensure(ctx, ctx->partial, (size_t)(ctx->Mp / nas::COST_BM) * ctx->Pp * KC * 8));
+    OK(nas::ensure(ctx, ctx->cand_key, (size_t)ctx->Pp * KC * 8));
+    OK(nas::ensure(ctx, ctx->cand_node, (size_t)ctx->Pp * KC * 4));
+    OK(nas::ensure(ctx, ctx->cand_cnt, (size_t)ctx->Pp * 4));
+    OK(nas::ensure(ctx, ctx->out_node, (size_t)ctx->Pp * 4));
+    OK(nas::ensure(ctx, ctx->out_cost_i, (size_t)ctx->Pp * 4));
+    OK(nas::ensure(ctx, ctx->status, 256));
+    if (ctx->world > 1) OK(nas::ensure(ctx, ctx->gather, (size_t)ctx->world * ctx->Pp * KC * 8));
+    if (!ctx->host_status.p) {
+        HIPCK(hipHostMalloc(&ctx->host_status.p, 256, hipHostMallocDefault));
+        ctx->host_status.bytes = 256;
+    }
+    return NAS_OK;
+}
+
+float decode_cost(uint32_t raw, int dtype) {
+    if (dtype == NAS_DT_I8) return (float)(int32_t)(raw ^ 0x80000000u);
+    const uint32_t u = (raw & 0x80000000u) ? (raw & 0x7fffffffu) : ~raw;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nas_version(void) { return NAS_ABI_VERSION; }
+
+int nas_create(nas_ctx **out, const nas_config *cfg) {
+    if (!out) return NAS_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) return NAS_ERR_HIP;
+    const int dev = cfg ? cfg->device : 0;
+    if (dev < 0 || dev >= ndev) return NAS_ERR_ARG;
+    nas_ctx *ctx = new (std::nothrow) nas_ctx();
+    if (!ctx) return NAS_ERR_NOMEM;
+    ctx->device = dev;
+    if (hipSetDevice(dev) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return NAS_ERR_HIP;
+    }
+    *out = ctx;
+    return NAS_OK;
+}
+
+void nas_destroy(nas_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    DevBuf *bufs[] = {&ctx->snap[0], &ctx->snap[1], &ctx->snap[2], &ctx->snap[3], &ctx->snap[4],
+                      &ctx->snap[5], &ctx->order1, &ctx->pos1, &ctx->order2, &ctx->pos2,
+                      &ctx->pod_snap, &ctx->best, &ctx->winners, &ctx->snap_best, &ctx->snap_win,
+                      &ctx->Lt, &ctx->WA, &ctx->cap0, &ctx->cap, &ctx->req, &ctx->mask,
+                      &ctx->partial, &ctx->cand_key, &ctx->gather, &ctx->cand_node,
+                      &ctx->cand_cnt, &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
+                      &ctx->status, &ctx->scratch};
+    for (DevBuf *b : bufs)
+        if (b->p) (void)hipFree(b->p);
+    if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
+    if (ctx->comm) (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(ctx->comm));
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *nas_last_error(nas_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int nas_get_timings(nas_ctx *ctx, nas_timings *out) {
+    if (!ctx || !out) return NAS_ERR_ARG;
+    *out = ctx->timings;
+    return NAS_OK;
+}
+
+// ---------------------------------------------------------------- reference
+int nas_upload_snapshot(nas_ctx *ctx, const double *cpu, const double *mem, const int64_t *rx,
+                        const int64_t *tx, const double *bw, const int64_t *disk, int32_t n_nodes,
+                        int32_t n_snapshots) {
+    OK(bind(ctx));
+    if (!cpu || !mem || !rx || !tx || !bw || !disk || n_nodes <= 0 || n_snapshots <= 0)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_snapshot: null array or empty size");
+    const int64_t ns = nas::round_up(n_nodes, 2);
+    const void *src[6] = {cpu, mem, bw, rx, tx, disk};
+    for (int f = 0; f < 6; ++f) {
+        OK(nas::ensure(ctx, ctx->snap[f], (size_t)ns * n_snapshots * 8));
+        HIPCK(hipMemcpy2DAsync(ctx->snap[f].p, ns * 8, src[f], (size_t)n_nodes * 8,
+                               (size_t)n_nodes * 8, n_snapshots, hipMemcpyHostToDevice,
+                               ctx->stream));
+    }
+    if (ctx->snap_n != n_nodes) ctx->n_orders = 0;  // orders no longer match
+    ctx->snap_n = n_nodes;
+    ctx->snap_s = n_snapshots;
+    ctx->snap_ns = ns;
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    return NAS_OK;
+}
+
+int nas_upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
+                      int32_t n_orders) {
+    OK(bind(ctx));
+    return upload_orders(ctx, order1, order2, n_orders);
+}
+
+int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
+                        const int32_t *pod_snapshot, int32_t P, int32_t *best_out,
+                        int32_t *winners_out) {
+    OK(bind(ctx));
+    if (ctx->snap_s <= 0) return nas::fail(ctx, NAS_ERR_STATE, "no snapshot uploaded");
+    if (P < 0 || (P > 0 && !best_out)) return nas::fail(ctx, NAS_ERR_ARG, "P / best_out");
+    if ((order1 == nullptr) != (order2 == nullptr))
+        return nas::fail(ctx, NAS_ERR_ARG, "order1 and order2 must both be given or both NULL");
+    if (order1) OK(upload_orders(ctx, order1, order2, 1));
+    if (ctx->n_orders != 1 && ctx->n_orders != ctx->snap_s)
+        return nas::fail(ctx, NAS_ERR_STATE, "orders: need 1 set or one per snapshot");
+    if (!pod_snapshot && P > ctx->snap_s)
+        return nas::fail(ctx, NAS_ERR_ARG, "pod_snapshot NULL needs P <= n_snapshots");
+    if (pod_snapshot)
+        for (int p = 0; p < P; ++p)
+            if (pod_snapshot[p] < 0 || pod_snapshot[p] >= ctx->snap_s)
+                return nas::fail(ctx, NAS_ERR_ARG, "pod_snapshot index out of range");
+    if (P == 0) return NAS_OK;
+    const int S = ctx->snap_s;
+    OK(nas::ensure(ctx, ctx->snap_best, (size_t)S * 4));
+    OK(nas::ensure(ctx, ctx->snap_win, (size_t)S * 6 * 4));
+    Timer tm(ctx);
+    std::memset(&ctx->timings, 0, sizeof(ctx->timings));
+    hipEvent_t a = tm.mark();
+    HIPCK(nas::launch_vote(ctx->stream, ctx, pod_snapshot ? S : P));
+    hipEvent_t b = tm.mark();
+    const int32_t *best_d = ctx->snap_best.as<int32_t>();
+    const int32_t *win_d = ctx->snap_win.as<int32_t>();
+    if (pod_snapshot) {
+        OK(nas::ensure(ctx, ctx->pod_snap, (size_t)P * 4));
+        OK(nas::ensure(ctx, ctx->best, (size_t)P * 4));
+        OK(nas::ensure(ctx, ctx->winners, (size_t)P * 24));
+        HIPCK(hipMemcpyAsync(ctx->pod_snap.p, pod_snapshot, (size_t)P * 4, hipMemcpyHostToDevice,
+                             ctx->stream));
+        HIPCK(nas::launch_vote_gather(ctx->stream, ctx->pod_snap.as<int32_t>(), P, best_d, win_d,
+                                      ctx->best.as<int32_t>(), ctx->winners.as<int32_t>()));
+        best_d = ctx->best.as<int32_t>();
+        win_d = ctx->winners.as<int32_t>();
+    }
+    HIPCK(hipMemcpyAsync(best_out, best_d, (size_t)P * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (winners_out)
+        HIPCK(hipMemcpyAsync(winners_out, win_d, (size_t)P * 24, hipMemcpyDeviceToHost, ctx->stream));
+    hipEvent_t c = tm.mark();
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    tm.span(T_VOTE, a, b);
+    tm.span(T_TOTAL, a, c);
+    ctx->timings.vote_ms = tm.total(T_VOTE);
+    ctx->timings.total_ms = tm.total(T_TOTAL);
+    return NAS_OK;
+}
+
+// ----------------------------------------------------------------- extended
+int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
+    OK(bind(ctx));
+    if (!L || n <= 0 || (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_latency: L / n / dtype");
+    if ((int64_t)n * 127 * 128 >= (int64_t)1 << 31 && dtype == NAS_DT_I8)
+        return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "int8 path: n too large for exact int32 costs");
+    if ((ctx->have_cap || ctx->have_pods || ctx->have_wa) && (ctx->N != n))
+        return nas::fail(ctx, NAS_ERR_ARG, "node count differs from earlier uploads");
+    if (ctx->have_wa && ctx->dtype != dtype)
+        return nas::fail(ctx, NAS_ERR_ARG, "dtype differs from the uploaded traffic");
+    set_geometry(ctx, n, dtype);
+    const size_t e = esz(dtype);
+    OK(nas::ensure(ctx, ctx->Lt, (size_t)ctx->Mp * ctx->Kp * e));
+    DevBuf tmp;
+    OK(nas::ensure(ctx, tmp, (size_t)n * n * e));
+    hipError_t he = hipMemcpyAsync(tmp.p, L, (size_t)n * n * e, hipMemcpyHostToDevice, ctx->stream);
+    if (he == hipSuccess)
+        he = nas::launch_transpose_L(ctx->stream, tmp.p, dtype, n, ctx->Nloc0, ctx->Nloc, ctx->Mp,
+                                     ctx->Kp, ctx->Lt.p);
+    if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(tmp.p);
+    if (he != hipSuccess) return nas::hip_fail(ctx, he, "upload latency");
+    ctx->have_L = true;
+    ctx->synth_valid = false;
+    return NAS_OK;
+}
+
+int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *mem_kib,
+                        const int32_t *pods, int32_t n) {
+    OK(bind(ctx));
+    if (!cpu_milli || !mem_kib || !pods || n <= 0)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_capacity");
+    if ((ctx->have_L || ctx->have_pods || ctx->have_wa) && ctx->N != n)
+        return nas::fail(ctx, NAS_ERR_ARG, "node count differs from earlier uploads");
+    if (!ctx->have_L && !ctx->have_wa) set_geometry(ctx, n, ctx->dtype ? ctx->dtype : NAS_DT_I8);
+    OK(nas::ensure(ctx, ctx->cap0, (size_t)3 * n * 4));
+    OK(nas::ensure(ctx, ctx->cap, (size_t)3 * n * 4));
+    const int32_t *src[3] = {cpu_milli, mem_kib, pods};
+    for (int r = 0; r < 3; ++r)
+        HIPCK(hipMemcpyAsync(ctx->cap0.as<int32_t>() + (size_t)r * n, src[r], (size_t)n * 4,
+                             hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * n * 4, hipMemcpyDeviceToDevice,
+                         ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->N = n;
+    ctx->have_cap = true;
+    return NAS_OK;
+}
+
+int nas_reset_capacity(nas_ctx *ctx) {
+    OK(bind(ctx));
+    if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
+    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * ctx->N * 4, hipMemcpyDeviceToDevice,
+                         ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    return NAS_OK;
+}
+
+int nas_get_capacity(nas_ctx *ctx, int32_t *cpu_milli, int32_t *mem_kib, int32_t *pods,
+                     int32_t n) {
+    OK(bind(ctx));
+    if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
+    if (n != ctx->N || !cpu_milli || !mem_kib || !pods)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_get_capacity");
+    int32_t *dst[3] = {cpu_milli, mem_kib, pods};
+    for (int r = 0; r < 3; ++r)
+        HIPCK(hipMemcpyAsync(dst[r], ctx->cap.as<int32_t>() + (size_t)r * n, (size_t)n * 4,
+                             hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    return NAS_OK;
+}
+
+int nas_upload_pods(nas_ctx *ctx, const int32_t *rc, const int32_t *rm, const int32_t *rp,
+                    int32_t P) {
+    OK(bind(ctx));
+    if (!rc || !rm || !rp || P <= 0) return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_pods");
+    if (ctx->have_wa && ctx->P != P)
+        return nas::fail(ctx, NAS_ERR_ARG, "pod count differs from the uploaded traffic");
+    for (int p = 0; p < P; ++p)
+        if (rc[p] < 0 || rm[p] < 0 || rp[p] < 0)
+            return nas::fail(ctx, NAS_ERR_ARG, "negative resource request");
+    const int Pp = (int)nas::round_up(P, nas::COST_BN);
+    std::vector<int32_t> h((size_t)3 * Pp, 0);
+    std::copy(rc, rc + P, h.begin());
+    std::copy(rm, rm + P, h.begin() + Pp);
+    std::copy(rp, rp + P, h.begin() + 2 * (size_t)Pp);
+    OK(nas::ensure(ctx, ctx->req, h.size() * 4));
+    HIPCK(hipMemcpyAsync(ctx->req.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->P = P;
+    ctx->Pp = Pp;
+    ctx->have_pods = true;
+    return NAS_OK;
+}
+
+static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
+    if (P <= 0 || n <= 0 || (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
+        return nas::fail(ctx, NAS_ERR_ARG, "traffic: P / n / dtype");
+    if ((ctx->have_L || ctx->have_cap) && ctx->N != n)
+        return nas::fail(ctx, NAS_ERR_ARG, "node count differs from earlier uploads");
+    if (ctx->have_L && ctx->dtype != dtype)
+        return nas::fail(ctx, NAS_ERR_ARG, "dtype differs from the uploaded latency");
+    if (ctx->have_pods && ctx->P != P)
+        return nas::fail(ctx, NAS_ERR_ARG, "pod count differs from the uploaded pods");
+    if (!ctx->have_L) set_geometry(ctx, n, dtype);
+    ctx->P = P;
+    ctx->Pp = (int32_t)nas::round_up(P, nas::COST_BN);
+    OK(nas::ensure(ctx, ctx->WA, (size_t)ctx->Pp * ctx->Kp * esz(dtype)));
+    HIPCK(hipMemsetAsync(ctx->WA.p, 0, (size_t)ctx->Pp * ctx->Kp * esz(dtype), ctx->stream));
+    return NAS_OK;
+}
+
+int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_t P, int32_t n) {
+    OK(bind(ctx));
+    if (!WA) return nas::fail(ctx, NAS_ERR_ARG, "WA null");
+    OK(traffic_common(ctx, dtype, P, n));
+    const size_t e = esz(dtype);
+    HIPCK(hipMemcpy2DAsync(ctx->WA.p, (size_t)ctx->Kp * e, WA, (size_t)n * e, (size_t)n * e, P,
+                           hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->have_wa = true;
+    ctx->synth_valid = false;
+    return NAS_OK;
+}
+
+int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *peer_node,
+                           const void *weight, int32_t dtype, int32_t P, int32_t n, int64_t nnz) {
+    OK(bind(ctx));
+    if (!row_ptr || nnz < 0 || (nnz > 0 && (!peer_node || !weight)))
+        return nas::fail(ctx, NAS_ERR_ARG, "csr arrays");
+    if (row_ptr[0] != 0 || row_ptr[P] != nnz) return nas::fail(ctx, NAS_ERR_ARG, "row_ptr bounds");
+    for (int p = 0; p < P; ++p)
+        if (row_ptr[p + 1] < row_ptr[p]) return nas::fail(ctx, NAS_ERR_ARG, "row_ptr not monotone");
+    OK(traffic_common(ctx, dtype, P, n));
+    DevBuf rp, pn, w;
+    int rc = nas::ensure(ctx, rp, (size_t)(P + 1) * 4);
+    if (rc == NAS_OK) rc = nas::ensure(ctx, pn, (size_t)nnz * 4);
+    if (rc == NAS_OK) rc = nas::ensure(ctx, w, (size_t)nnz * esz(dtype));
+    hipError_t he = hipSuccess;
+    if (rc == NAS_OK) {
+        he = hipMemcpyAsync(rp.p, row_ptr, (size_t)(P + 1) * 4, hipMemcpyHostToDevice, ctx->stream);
+        if (he == hipSuccess && nnz)
+            he = hipMemcpyAsync(pn.p, peer_node, (size_t)nnz * 4, hipMemcpyHostToDevice, ctx->stream);
+        if (he == hipSuccess && nnz)
+            he = hipMemcpyAsync(w.p, weight, (size_t)nnz * esz(dtype), hipMemcpyHostToDevice,
+                                ctx->stream);
+        if (he == hipSuccess)
+            he = nas::launch_csr_aggregate(ctx->stream, rp.as<int32_t>(), pn.as<int32_t>(), w.p,
+                                           dtype, P, n, ctx->Kp, ctx->WA.p);
+        if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+    }
+    (void)hipStreamSynchronize(ctx->stream);
+    for (DevBuf *b : {&rp, &pn, &w})
+        if (b->p) (void)hipFree(b->p);
+    if (rc != NAS_OK) return rc;
+    if (he != hipSuccess) return nas::hip_fail(ctx, he, "csr aggregate");
+    ctx->have_wa = true;
+    ctx->synth_valid = false;
+    return NAS_OK;
+}
+
+int nas_filter(nas_ctx *ctx, uint64_t *mask_out) {
+    OK(bind(ctx));
+    if (!ctx->have_cap || !ctx->have_pods || ctx->N <= 0)
+        return nas::fail(ctx, NAS_ERR_STATE, "nas_filter needs capacity and pods");
+    OK(alloc_extended(ctx));
+    Timer tm(ctx);
+    hipEvent_t a = tm.mark();
+    HIPCK(nas::launch_fit(ctx->stream, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc,
+                          ctx->Mp, ctx->req.as<int32_t>(), ctx->P, ctx->Pp, 0, ctx->P,
+                          ctx->mask.as<uint64_t>()));
+    hipEvent_t b = tm.mark();
+    if (mask_out) {
+        const int chunks = (ctx->Nloc + 63) / 64;
+        HIPCK(hipMemcpy2DAsync(mask_out, (size_t)ctx->P * 8, ctx->mask.p, (size_t)ctx->Pp * 8,
+                               (size_t)ctx->P * 8, chunks, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    tm.span(T_FIT, a, b);
+    ctx->timings.fit_ms = tm.total(T_FIT);
+    return NAS_OK;
+}
+
+int nas_score(nas_ctx *ctx) {
+    OK(bind(ctx));
+    OK(check_extended(ctx));
+    OK(alloc_extended(ctx));
+    std::memset(&ctx->timings, 0, sizeof(ctx->timings));
+    Timer tm(ctx);
+    OK(score_range(ctx, tm, 0, ctx->P));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->timings.fit_ms = tm.total(T_FIT);
+    ctx->timings.cost_ms = tm.total(T_COST);
+    ctx->timings.merge_ms = tm.total(T_MERGE);
+    ctx->scored = true;
+    return NAS_OK;
+}
+
+int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_score_out) {
+    OK(bind(ctx));
+    OK(check_extended(ctx));
+    if (!node_out) return nas::fail(ctx, NAS_ERR_ARG, "node_out null");
+    OK(alloc_extended(ctx));
+    std::memset(&ctx->timings, 0, sizeof(ctx->timings));
+    Timer tm(ctx);
+    hipStream_t st = ctx->stream;
+    hipEvent_t t0 = tm.mark();
+    OK(score_range(ctx, tm, 0, ctx->P));
+    int32_t *hs = ctx->host_status.as<int32_t>();
+    int p = 0, rounds = 0;
+    while (true) {
+        hipEvent_t c0 = tm.mark();
+        HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_cnt.as<int32_t>(),
+                                 ctx->req.as<int32_t>(), ctx->Pp, p, ctx->P, ctx->cap.as<int32_t>(),
+                                 ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
+                                 ctx->status.as<int32_t>()));
+        hipEvent_t c1 = tm.mark();
+        tm.span(T_COMMIT, c0, c1);
+        HIPCK(hipMemcpyAsync(hs, ctx->status.p, 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+        const int stop = hs[0];
+        if (stop < p || stop > ctx->P) return nas::fail(ctx, NAS_ERR_HIP, "commit status corrupt");
+        if (stop >= ctx->P) break;
+        // pod `stop` exhausted its candidates: rescore a window against the
+        // current capacity (lists computed now stay valid for later pods)
+        ++rounds;
+        if (rounds > ctx->P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
+        OK(score_range(ctx, tm, stop, std::min(ctx->P, stop + RESCORE_PODS)));
+        p = stop;
+    }
+    const int P = ctx->P;
+    std::vector<uint32_t> raw;
+    HIPCK(hipMemcpyAsync(node_out, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+    if (cost_out || int_score_out) {
+        raw.resize(P);
+        HIPCK(hipMemcpyAsync(raw.data(), ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+    }
+    hipEvent_t t1 = tm.mark();
+    HIPCK(hipStreamSynchronize(st));
+    tm.span(T_TOTAL, t0, t1);
+    int unsched = 0;
+    for (int i = 0; i < P; ++i) {
+        const bool none = node_out[i] < 0;
+        unsched += none;
+        if (cost_out) cost_out[i] = none ? 0.f : decode_cost(raw[i], ctx->dtype);
+        if (int_score_out)
+            int_score_out[i] = (none || ctx->dtype != NAS_DT_I8) ? 0
+                                                                : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
+    }
+    ctx->timings.fit_ms = tm.total(T_FIT);
+    ctx->timings.cost_ms = tm.total(T_COST);
+    ctx->timings.merge_ms = tm.total(T_MERGE);
+    ctx->timings.commit_ms = tm.total(T_COMMIT);
+    ctx->timings.total_ms = tm.total(T_TOTAL);
+    ctx->timings.rescore_rounds = rounds;
+    ctx->timings.unschedulable = unsched;
+    ctx->scored = true;
+    return NAS_OK;
+}
+
+int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i, float *cand_cost_f,
+                       int32_t *count) {
+    OK(bind(ctx));
+    if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
+    const int P = ctx->P;
+    std::vector<uint64_t> keys((size_t)P * KC);
+    HIPCK(hipMemcpyAsync(keys.data(), ctx->cand_key.p, keys.size() * 8, hipMemcpyDeviceToHost,
+                         ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    for (int p = 0; p < P; ++p) {
+        int c = 0;
+        for (int j = 0; j < KC; ++j) {
+            const uint64_t k = keys[(size_t)p * KC + j];
+            const bool ok = k != nas::KEY_INVALID;
+            c += ok;
+            if (cand_node) cand_node[(size_t)p * KC + j] = ok ? (int32_t)(uint32_t)k : -1;
+            const uint32_t raw = (uint32_t)(k >> 32);
+            if (cand_cost_i)
+                cand_cost_i[(size_t)p * KC + j] =
+                    (ok && ctx->dtype == NAS_DT_I8) ? (int64_t)(int32_t)(raw ^ 0x80000000u) : 0;
+            if (cand_cost_f) cand_cost_f[(size_t)p * KC + j] = ok ? decode_cost(raw, ctx->dtype) : 0.f;
+        }
+        if (count) count[p] = c;
+    }
+    return NAS_OK;
+}
+
+// ---------------------------------------------------------------- multi-GPU
+int nas_comm_unique_id(uint8_t id_out[128]) {
+    if (!id_out) return NAS_ERR_ARG;
+    ncclUniqueId id;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    if (ncclGetUniqueId(&id) != ncclSuccess) return NAS_ERR_COMM;
+    std::memcpy(id_out, &id, 128);
+    return NAS_OK;
+}
+
+int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world) {
+    OK(bind(ctx));
+    if (!id || world < 1 || rank < 0 || rank >= world)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_comm_init: rank/world");
+    if (ctx->have_L || ctx->have_wa || ctx->have_cap)
+        return nas::fail(ctx, NAS_ERR_STATE, "nas_comm_init must precede the extended uploads");
+    if (ctx->comm) {
+        (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(ctx->comm));
+        ctx->comm = nullptr;
+    }
+    ctx->rank = rank;
+    ctx->world = world;
+    if (world == 1) return NAS_OK;
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    ncclComm_t comm;
+    ncclResult_t r = ncclCommInitRank(&comm, world, uid, rank);
+    if (r != ncclSuccess)
+        return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    ctx->comm = reinterpret_cast<ncclComm *>(comm);
+    return NAS_OK;
+}
+
+// ---------------------------------------------------------------- synthetic
+int nas_synth_snapshots(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t n_snapshots) {
+    OK(bind(ctx));
+    if (n_nodes <= 0 || n_snapshots <= 0) return nas::fail(ctx, NAS_ERR_ARG, "synth sizes");
+    const int64_t ns = nas::round_up(n_nodes, 2);
+    for (int f = 0; f < 6; ++f) OK(nas::ensure(ctx, ctx->snap[f], (size_t)ns * n_snapshots * 8));
+    HIPCK(nas::launch_synth_snapshots(ctx->stream, seed, n_nodes, ns, n_snapshots,
+                                      ctx->snap[0].as<double>(), ctx->snap[1].as<double>(),
+                                      ctx->snap[2].as<double>(), ctx->snap[3].as<int64_t>(),
+                                      ctx->snap[4].as<int64_t>(), ctx->snap[5].as<int64_t>()));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    if (ctx->snap_n != n_nodes) ctx->n_orders = 0;
+    ctx->snap_n = n_nodes;
+    ctx->snap_s = n_snapshots;
+    ctx->snap_ns = ns;
+    return NAS_OK;
+}
+
+int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t *rx, int64_t *tx,
+                      double *bw, int64_t *disk) {
+    OK(bind(ctx));
+    if (s < 0 || s >= ctx->snap_s) return nas::fail(ctx, NAS_ERR_ARG, "snapshot index");
+    void *dst[6] = {cpu, mem, bw, rx, tx, disk};
+    for (int f = 0; f < 6; ++f) {
+        if (!dst[f]) continue;
+        HIPCK(hipMemcpyAsync(dst[f], ctx->snap[f].as<char>() + (size_t)s * ctx->snap_ns * 8,
+                             (size_t)ctx->snap_n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    return NAS_OK;
+}
+
+int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, int32_t dtype,
+                      int32_t peers) {
+    OK(bind(ctx));
+    if (n_nodes <= 0 || P <= 0 || peers < 1 || peers > 16 ||
+        (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_synth_cluster arguments");
+    set_geometry(ctx, n_nodes, dtype);
+    ctx->P = P;
+    ctx->Pp = (int32_t)nas::round_up(P, nas::COST_BN);
+    const size_t e = esz(dtype);
+    OK(nas::ensure(ctx, ctx->Lt, (size_t)ctx->Mp * ctx->Kp * e));
+    OK(nas::ensure(ctx, ctx->WA, (size_t)ctx->Pp * ctx->Kp * e));
+    OK(nas::ensure(ctx, ctx->cap0, (size_t)3 * n_nodes * 4));
+    OK(nas::ensure(ctx, ctx->cap, (size_t)3 * n_nodes * 4));
+    OK(nas::ensure(ctx, ctx->req, (size_t)3 * ctx->Pp * 4));
+    HIPCK(nas::launch_synth_cluster(ctx->stream, seed, n_nodes, P, dtype, peers, ctx->Nloc0,
+                                    ctx->Nloc, ctx->Mp, ctx->Kp, ctx->Pp, ctx->Lt.p, ctx->WA.p,
+                                    ctx->cap0.as<int32_t>(), ctx->req.as<int32_t>(), nullptr));
+    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * n_nodes * 4, hipMemcpyDeviceToDevice,
+                         ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->have_L = ctx->have_cap = ctx->have_pods = ctx->have_wa = true;
+    ctx->synth_valid = true;
+    ctx->synth_seed = seed;
+    return NAS_OK;
+}
+
+int nas_read_inputs(nas_ctx *ctx, int32_t p0, int32_t np, void *WA_rows, void *L, int32_t *cap_cpu,
+                    int32_t *cap_mem, int32_t *cap_pods, int32_t *req_cpu, int32_t *req_mem,
+                    int32_t *req_pods) {
+    OK(bind(ctx));
+    OK(check_extended(ctx));
+    const int N = ctx->N;
+    const size_t e = esz(ctx->dtype);
+    if (WA_rows) {
+        if (p0 < 0 || np < 0 || p0 + np > ctx->P) return nas::fail(ctx, NAS_ERR_ARG, "pod rows");
+        if (np)
+            HIPCK(hipMemcpy2DAsync(WA_rows, (size_t)N * e, ctx->WA.as<char>() + (size_t)p0 * ctx->Kp * e,
+                                   (size_t)ctx->Kp * e, (size_t)N * e, np, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    }
+    if (L) {
+        if (ctx->synth_valid) {
+            DevBuf tmp;
+            OK(nas::ensure(ctx, tmp, (size_t)N * N * e));
+            hipError_t he = nas::launch_synth_cluster(ctx->stream, ctx->synth_seed, N, ctx->P,
+                                                      ctx->dtype, 1, 0, 0, 0, 0, 0, nullptr,
+                                                      nullptr, nullptr, nullptr, tmp.p);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(L, tmp.p, (size_t)N * N * e, hipMemcpyDeviceToHost, ctx->stream);
+            if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+            (void)hipFree(tmp.p);
+            if (he != hipSuccess) return nas::hip_fail(ctx, he, "read L");
+        } else if (ctx->world == 1) {
+            std::vector<char> lt((size_t)N * ctx->Kp * e);
+            HIPCK(hipMemcpyAsync(lt.data(), ctx->Lt.p, lt.size(), hipMemcpyDeviceToHost, ctx->stream));
+            HIPCK(hipStreamSynchronize(ctx->stream));
+            char *out = static_cast<char *>(L);
+            for (int i = 0; i < N; ++i)
+                for (int m = 0; m < N; ++m)
+                    std::memcpy(out + ((size_t)m * N + i) * e, lt.data() + ((size_t)i * ctx->Kp + m) * e, e);
+        } else {
+            return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "full L is not resident on a sharded rank");
+        }
+    }
+    int32_t *cdst[3] = {cap_cpu, cap_mem, cap_pods};
+    for (int r = 0; r < 3; ++r)
+        if (cdst[r])
+            HIPCK(hipMemcpyAsync(cdst[r], ctx->cap0.as<int32_t>() + (size_t)r * N, (size_t)N * 4,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    int32_t *rdst[3] = {req_cpu, req_mem, req_pods};
+    for (int r = 0; r < 3; ++r)
+        if (rdst[r])
+            HIPCK(hipMemcpyAsync(rdst[r], ctx->req.as<int32_t>() + (size_t)r * ctx->Pp,
+                                 (size_t)ctx->P * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    return NAS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,128 @@
+// nas_internal.h -- context, device buffers and kernel launch interfaces of
+// the MI355X placement engine (gfx950 only).  See DESIGN.md for the data
+// layout in HBM and the roofline of each kernel.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/nas.h"
+
+struct ncclComm;
+
+namespace nas {
+
+constexpr int KC = NAS_K_CANDIDATES;  // candidates per pod
+
+// Cost contraction tile (see k_cost.hip): BM nodes x BN pods, 128-byte K stage.
+constexpr int COST_BM = 256;
+constexpr int COST_BN = 256;
+constexpr int COST_BKB = 128;  // bytes of K per stage (128 int8 or 64 bf16)
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    template <typename T>
+    T *as() const { return static_cast<T *>(p); }
+};
+
+// packed candidate key: orderable 32-bit cost in the high word, node index
+// in the low word; ascending key == ascending (cost, node).
+constexpr uint64_t KEY_INVALID = ~0ull;
+
+}  // namespace nas
+
+struct nas_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    hipEvent_t ev[12] = {};
+    nas_timings timings = {};
+
+    // ---- reference mode
+    int32_t snap_n = 0, snap_s = 0;   // nodes, snapshots
+    int64_t snap_ns = 0;              // padded row stride (even)
+    nas::DevBuf snap[6];              // cpu, mem, bw (f64) ; rx, tx, disk (i64)  [S][ns]
+    int32_t n_orders = 0;
+    int64_t ord_ns = 0;               // row stride of order arrays
+    nas::DevBuf order1, pos1;         // [n_orders][ord_ns]
+    nas::DevBuf order2, pos2;         // [n_orders][ord_ns + 2]  (n+1 keys)
+    nas::DevBuf pod_snap, best, winners;
+    nas::DevBuf snap_best, snap_win;  // per-snapshot results
+
+    // ---- extended mode
+    int32_t N = 0;           // nodes
+    int32_t P = 0;           // pending pods
+    int32_t dtype = 0;       // element type of L and WA
+    int32_t Kp = 0;          // padded contraction length (row bytes / elt)
+    int32_t Nloc0 = 0, Nloc = 0;  // node shard [Nloc0, Nloc0+Nloc) owned by this rank
+    int32_t Mp = 0;          // padded local node count (multiple of COST_BM)
+    int32_t Pp = 0;          // padded pod count (multiple of COST_BN)
+    bool have_L = false, have_cap = false, have_pods = false, have_wa = false;
+    nas::DevBuf Lt;          // [Mp][Kp] elements: Lt[i][m] = L[m][Nloc0 + i]
+    nas::DevBuf WA;          // [Pp][Kp] elements
+    nas::DevBuf cap0, cap;   // [3][N] int32 (initial, working)
+    nas::DevBuf req;         // [3][Pp] int32
+    nas::DevBuf mask;        // [ceil(Mp/64)][Pp] uint64, local nodes
+    nas::DevBuf partial;     // [Mp/BM][Pp][KC] uint64 keys
+    nas::DevBuf cand_key;    // [Pp][KC] uint64 (global node ids), after merge
+    nas::DevBuf gather;      // [world][Pp][KC] uint64 (multi-GPU exchange)
+    nas::DevBuf cand_node;   // [Pp][KC] int32
+    nas::DevBuf cand_cnt;    // [Pp] int32
+    nas::DevBuf out_node, out_cost_f, out_cost_i;  // [Pp]
+    nas::DevBuf status;      // small device scratch for commit control
+    nas::DevBuf host_status; // pinned
+    nas::DevBuf scratch;
+    bool scored = false;        // a scoring pass filled cand_key
+    bool synth_valid = false;   // inputs came from nas_synth_cluster(synth_seed)
+    uint64_t synth_seed = 0;
+
+    // ---- multi-GPU
+    ncclComm *comm = nullptr;
+    int32_t rank = 0, world = 1;
+};
+
+namespace nas {
+
+int fail(nas_ctx *ctx, int code, const std::string &msg);
+int hip_fail(nas_ctx *ctx, hipError_t e, const char *what);
+int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes);
+
+// kernel launchers (k_*.hip); all enqueue on `stream` and return hipError_t
+hipError_t launch_vote(hipStream_t st, const nas_ctx *c, int n_snapshots_used);
+hipError_t launch_vote_gather(hipStream_t st, const int32_t *pod_snap, int P,
+                              const int32_t *snap_best, const int32_t *snap_win, int32_t *best,
+                              int32_t *win);
+
+hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nloc, int Mp,
+                      const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask);
+
+hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
+                            int Kp, int Pp, int p0, int np, const uint64_t *mask,
+                            uint64_t *partial, int node_base);
+hipError_t launch_merge(hipStream_t st, const uint64_t *partial, int n_lists, int64_t list_stride,
+                        int src_p0, int p0, int np, uint64_t *cand_key);
+hipError_t launch_unpack(hipStream_t st, const uint64_t *cand_key, int p0, int np, int dtype,
+                         int32_t *cand_node, int32_t *cand_cnt);
+hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const int32_t *cand_cnt,
+                         const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
+                         int32_t *out_node, int32_t *out_cost_i, int32_t *status);
+
+hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
+                              int nloc, int Mp, int Kp, void *Lt);
+hipError_t launch_csr_aggregate(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
+                                const void *w, int dtype, int P, int N, int Kp, void *WA);
+
+hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int64_t ns, int S,
+                                  double *cpu, double *mem, double *bw, int64_t *rx, int64_t *tx,
+                                  int64_t *disk);
+hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
+                                int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
+                                int32_t *cap, int32_t *req, void *L_full /* optional N*N */);
+
+}  // namespace nas

@@ -1,0 +1,205 @@
+"""Engine: a numpy-facing handle on one nas_ctx (one HIP device).
+
+Thin plumbing over the C ABI for tests and bench.py.  Names follow the
+reference: snapshots are PrometheusNodeMetrics records
+(scheduler/scheduler.go:24-32), `score_reference` is prioritize +
+findBestNode (:248-394), `place` is the network-aware filter/score/commit.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import NasError, as_c, ptr
+
+FIELDS = ("cpu", "mem", "rx", "tx", "bw", "disk")
+_FDT = {"cpu": np.float64, "mem": np.float64, "rx": np.int64, "tx": np.int64,
+        "bw": np.float64, "disk": np.int64}
+
+
+class Engine:
+    def __init__(self, device=0):
+        self._L = _lib.lib()
+        cfg = _lib.NasConfig(device=device)
+        h = ctypes.c_void_p()
+        rc = self._L.nas_create(ctypes.byref(h), ctypes.byref(cfg))
+        if rc != 0:
+            raise NasError(rc, "nas_create failed (no GPU visible or bad device ordinal)")
+        self._h = h
+        self.n_nodes = 0
+        self.n_pods = 0
+        self.dtype = 0
+
+    # ------------------------------------------------------------ plumbing
+    def _ck(self, rc):
+        if rc != 0:
+            raise NasError(rc, self._L.nas_last_error(self._h).decode())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.nas_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def timings(self):
+        t = _lib.NasTimings()
+        self._ck(self._L.nas_get_timings(self._h, ctypes.byref(t)))
+        return t.as_dict()
+
+    # ------------------------------------------------------ reference mode
+    def upload_snapshot(self, snap):
+        """snap: dict of FIELDS -> (n_snapshots, n_nodes) or (n_nodes,) arrays."""
+        arrs = {f: as_c(snap[f], _FDT[f]) for f in FIELDS}
+        a0 = arrs["cpu"]
+        if a0.ndim == 1:
+            arrs = {f: a.reshape(1, -1) for f, a in arrs.items()}
+        S, n = arrs["cpu"].shape
+        for a in arrs.values():
+            if a.shape != (S, n):
+                raise ValueError("snapshot fields must share one shape")
+        self._ck(self._L.nas_upload_snapshot(self._h, ptr(arrs["cpu"]), ptr(arrs["mem"]),
+                                             ptr(arrs["rx"]), ptr(arrs["tx"]), ptr(arrs["bw"]),
+                                             ptr(arrs["disk"]), n, S))
+        self.snap_nodes, self.snap_count = n, S
+
+    def upload_orders(self, order1, order2):
+        o1 = as_c(order1, np.int32)
+        o2 = as_c(order2, np.int32)
+        n_orders = 1 if o1.ndim == 1 else o1.shape[0]
+        self._ck(self._L.nas_upload_orders(self._h, ptr(o1), ptr(o2), n_orders))
+
+    def score_reference(self, P=None, order1=None, order2=None, pod_snapshot=None, winners=True):
+        ps = None if pod_snapshot is None else as_c(pod_snapshot, np.int32)
+        if P is None:
+            P = self.snap_count if ps is None else ps.shape[0]
+        o1 = None if order1 is None else as_c(order1, np.int32)
+        o2 = None if order2 is None else as_c(order2, np.int32)
+        best = np.empty(P, np.int32)
+        win = np.empty((P, 6), np.int32) if winners else None
+        self._ck(self._L.nas_score_reference(self._h, ptr(o1), ptr(o2), ptr(ps), P, ptr(best),
+                                             ptr(win)))
+        return best, win
+
+    def synth_snapshots(self, seed, n_nodes, n_snapshots):
+        self._ck(self._L.nas_synth_snapshots(self._h, seed, n_nodes, n_snapshots))
+        self.snap_nodes, self.snap_count = n_nodes, n_snapshots
+
+    def read_snapshot(self, s):
+        n = self.snap_nodes
+        out = {f: np.empty(n, _FDT[f]) for f in FIELDS}
+        self._ck(self._L.nas_read_snapshot(self._h, s, ptr(out["cpu"]), ptr(out["mem"]),
+                                           ptr(out["rx"]), ptr(out["tx"]), ptr(out["bw"]),
+                                           ptr(out["disk"])))
+        return out
+
+    # -------------------------------------------------------- extended mode
+    def comm_init(self, uid, rank, world):
+        b = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        self._ck(self._L.nas_comm_init(self._h, b, rank, world))
+
+    @staticmethod
+    def comm_unique_id():
+        b = (ctypes.c_uint8 * 128)()
+        rc = _lib.lib().nas_comm_unique_id(b)
+        if rc != 0:
+            raise NasError(rc, "ncclGetUniqueId failed")
+        return bytes(b)
+
+    @staticmethod
+    def _dt(dtype):
+        return {"i8": _lib.NAS_DT_I8, "bf16": _lib.NAS_DT_BF16}[dtype]
+
+    @staticmethod
+    def _np(dtype):
+        return np.int8 if dtype == "i8" else np.uint16
+
+    def upload_latency(self, L, dtype):
+        L = as_c(L, self._np(dtype))
+        n = L.shape[0]
+        self._ck(self._L.nas_upload_latency(self._h, ptr(L), self._dt(dtype), n))
+        self.n_nodes, self.dtype = n, dtype
+
+    def upload_capacity(self, free):
+        free = as_c(free, np.int32)
+        cols = [np.ascontiguousarray(free[:, i]) for i in range(3)]
+        self._ck(self._L.nas_upload_capacity(self._h, *[ptr(c) for c in cols], free.shape[0]))
+        self.n_nodes = free.shape[0]
+
+    def reset_capacity(self):
+        self._ck(self._L.nas_reset_capacity(self._h))
+
+    def get_capacity(self):
+        n = self.n_nodes
+        cols = [np.empty(n, np.int32) for _ in range(3)]
+        self._ck(self._L.nas_get_capacity(self._h, *[ptr(c) for c in cols], n))
+        return np.stack(cols, axis=1)
+
+    def upload_pods(self, req):
+        req = as_c(req, np.int32)
+        cols = [np.ascontiguousarray(req[:, i]) for i in range(3)]
+        self._ck(self._L.nas_upload_pods(self._h, *[ptr(c) for c in cols], req.shape[0]))
+        self.n_pods = req.shape[0]
+
+    def upload_traffic(self, WA, dtype):
+        WA = as_c(WA, self._np(dtype))
+        P, n = WA.shape
+        self._ck(self._L.nas_upload_traffic_dense(self._h, ptr(WA), self._dt(dtype), P, n))
+        self.n_pods, self.n_nodes, self.dtype = P, n, dtype
+
+    def upload_traffic_csr(self, row_ptr, peer_node, weight, dtype, n):
+        rp = as_c(row_ptr, np.int32)
+        pn = as_c(peer_node, np.int32)
+        w = as_c(weight, self._np(dtype))
+        P = rp.shape[0] - 1
+        self._ck(self._L.nas_upload_traffic_csr(self._h, ptr(rp), ptr(pn), ptr(w), self._dt(dtype),
+                                                P, n, pn.shape[0]))
+        self.n_pods, self.n_nodes, self.dtype = P, n, dtype
+
+    def filter(self):
+        chunks = (self.n_nodes + 63) // 64
+        mask = np.zeros((chunks, self.n_pods), np.uint64)
+        self._ck(self._L.nas_filter(self._h, ptr(mask)))
+        return mask
+
+    def score(self):
+        self._ck(self._L.nas_score(self._h))
+
+    def candidates(self):
+        P, K = self.n_pods, _lib.K_CANDIDATES
+        node = np.empty((P, K), np.int32)
+        ci = np.empty((P, K), np.int64)
+        cf = np.empty((P, K), np.float32)
+        cnt = np.empty(P, np.int32)
+        self._ck(self._L.nas_get_candidates(self._h, ptr(node), ptr(ci), ptr(cf), ptr(cnt)))
+        return node, ci, cf, cnt
+
+    def place(self, want_cost=True):
+        P = self.n_pods
+        node = np.empty(P, np.int32)
+        cf = np.empty(P, np.float32) if want_cost else None
+        ci = np.empty(P, np.int64) if want_cost else None
+        self._ck(self._L.nas_place(self._h, ptr(node), ptr(cf), ptr(ci)))
+        return node, cf, ci
+
+    def synth_cluster(self, seed, n_nodes, P, dtype="i8", peers=8):
+        self._ck(self._L.nas_synth_cluster(self._h, seed, n_nodes, P, self._dt(dtype), peers))
+        self.n_nodes, self.n_pods, self.dtype = n_nodes, P, dtype
+
+    def read_inputs(self, p0=0, np_=0, want_L=True):
+        n, P = self.n_nodes, self.n_pods
+        dt = self._np(self.dtype)
+        WA = np.empty((np_, n), dt) if np_ else None
+        L = np.empty((n, n), dt) if want_L else None
+        cap = [np.empty(n, np.int32) for _ in range(3)]
+        req = [np.empty(P, np.int32) for _ in range(3)]
+        self._ck(self._L.nas_read_inputs(self._h, p0, np_, ptr(WA), ptr(L), *[ptr(c) for c in cap],
+                                         *[ptr(r) for r in req]))
+        return WA, L, np.stack(cap, axis=1), np.stack(req, axis=1)

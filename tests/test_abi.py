@@ -1,0 +1,69 @@
+"""CPU tests of the C-ABI boundary: libnas.so loads, exports exactly what
+include/nas.h declares, and fails loudly (no CPU fallback) without a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from kubernetesnetawarescheduler_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared():
+    with open(os.path.join(ROOT, "include", "nas.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(nas_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    names = declared()
+    for must in ["nas_create", "nas_destroy", "nas_upload_snapshot", "nas_score_reference",
+                 "nas_upload_latency", "nas_upload_pods", "nas_upload_capacity", "nas_place",
+                 "nas_last_error", "nas_comm_init"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    missing = [n for n in declared() if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    assert sorted(_lib.SIGNATURES) == declared()
+
+
+def test_version():
+    assert _lib.lib().nas_version() == 1
+
+
+def test_create_fails_loudly_without_gpu():
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    rc = L.nas_create(ctypes.byref(h), ctypes.byref(_lib.NasConfig(device=0)))
+    if rc == 0:
+        L.nas_destroy(h)
+        pytest.skip("a GPU is visible here")
+    assert rc == _lib.NAS_ERR_HIP
+    assert not h.value
+
+
+def test_engine_raises_without_gpu():
+    from kubernetesnetawarescheduler_amd import Engine, NasError
+    try:
+        e = Engine(0)
+    except NasError as err:
+        assert err.code == _lib.NAS_ERR_HIP
+        return
+    e.close()
+    pytest.skip("a GPU is visible here")
+
+
+def test_null_context_is_an_argument_error():
+    L = _lib.lib()
+    assert L.nas_score(None) == _lib.NAS_ERR_ARG
+    assert L.nas_get_timings(None, None) == _lib.NAS_ERR_ARG
+    assert L.nas_last_error(None) == b"null context"

@@ -1,0 +1,193 @@
+"""GPU parity of the extended mode: fit filter (k_fit), MFMA cost + fused top-k
+(k_cost), merge, and greedy commit (k_commit) against the CPU oracle.
+
+int8 inputs: exact -- masks, candidate lists, integer costs, placements and
+the remaining capacity are bit-identical.  bf16 inputs: integer-valued bf16
+is exact too (products and fp32 sums stay below 2^24); general bf16 costs
+must be within REL_TOL of the fp64 oracle (the north star's 1e-5)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from util import bf16_bits_to_f64, cluster
+
+pytestmark = pytest.mark.gpu
+REL_TOL = 1e-5
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def upload(engine, WA, L, free, req, dtype):
+    engine.upload_latency(L, dtype)
+    engine.upload_capacity(free)
+    engine.upload_pods(req)
+    engine.upload_traffic(WA, dtype)
+
+
+def test_place_golden(engine):
+    with open(os.path.join(GOLD, "place_small.json")) as f:
+        g = json.load(f)
+    upload(engine, np.array(g["WA"], np.int8), np.array(g["L"], np.int8), np.array(g["free"]),
+           np.array(g["req"]), "i8")
+    node, cf, ci = engine.place()
+    assert node.tolist() == g["node"]
+    assert ci.tolist() == g["cost"]
+    assert engine.get_capacity().tolist() == g["free_after"]
+
+
+@pytest.mark.parametrize("P,N", [(1, 1), (3, 5), (300, 70), (257, 129), (1000, 300), (513, 1000)])
+def test_fit_mask(engine, P, N):
+    rng = np.random.default_rng(P * 7 + N)
+    WA, L, free, req = cluster(rng, P, N, cap_scale=0.05)
+    upload(engine, WA, L, free, req, "i8")
+    got = engine.filter()  # [ceil(N/64)][P] uint64, bit j <-> node 64c + j
+    want = oracle.fit_mask(req, free)  # [P][ceil(N/32)] uint32
+    for c in range(got.shape[0]):
+        lo = want[:, 2 * c].astype(np.uint64)
+        hi = want[:, 2 * c + 1].astype(np.uint64) if 2 * c + 1 < want.shape[1] else 0
+        assert (got[c] == (lo | (np.uint64(hi) << np.uint64(32)))).all()
+
+
+@pytest.mark.parametrize("P,N,lo,hi", [(256, 256, 0, 20), (300, 70, -20, 20), (1000, 1000, 0, 127),
+                                       (700, 1500, -128, 127), (2048, 4096, 0, 8)])
+def test_candidates_i8_exact(engine, P, N, lo, hi):
+    rng = np.random.default_rng(P + N)
+    WA, L, free, req = cluster(rng, P, N, lo=lo, hi=hi, cap_scale=0.1)
+    upload(engine, WA, L, free, req, "i8")
+    engine.score()
+    node, ci, cf, cnt = engine.candidates()
+    cost = oracle.cost(WA, L, "i8")
+    mask = oracle.fit_mask(req, free)
+    wn, wc, wcnt = oracle.topk(cost, mask, 4)
+    assert (cnt == wcnt).all()
+    assert (node == wn).all()
+    valid = wn >= 0
+    assert (ci[valid] == wc[valid]).all()
+
+
+@pytest.mark.parametrize("P,N,cap", [(500, 200, 0.3), (1200, 333, 0.05), (3000, 1000, 0.02),
+                                     (4096, 640, 0.01)])
+def test_place_i8_exact(engine, P, N, cap):
+    """Placements, integer scores and remaining capacity identical to the
+    sequential oracle -- including commit conflicts, rescore rounds and
+    unschedulable pods at tight capacity."""
+    rng = np.random.default_rng(P ^ N)
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=60, cap_scale=cap)
+    # make locality strong so many pods want the same few nodes
+    WA[:, : N // 10] = np.minimum(WA[:, : N // 10].astype(np.int32) + 60, 127).astype(np.int8)
+    upload(engine, WA, L, free, req, "i8")
+    node, cf, ci = engine.place()
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    assert node.tolist() == want.tolist()
+    assert ci.tolist() == wcost.tolist()
+    assert (engine.get_capacity() == wfree).all()
+    t = engine.timings()
+    assert t["unschedulable"] == int((want < 0).sum())
+
+
+def test_rescore_path_runs(engine):
+    rng = np.random.default_rng(77)
+    P, N = 2000, 256
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=30, cap_scale=0.02)
+    WA[:, :8] = 127  # everyone wants nodes 0..7
+    upload(engine, WA, L, free, req, "i8")
+    node, _, ci = engine.place()
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    assert engine.timings()["rescore_rounds"] > 0
+    assert node.tolist() == want.tolist() and ci.tolist() == wcost.tolist()
+    assert (engine.get_capacity() == wfree).all()
+
+
+@pytest.mark.parametrize("P,N", [(300, 200), (1000, 700)])
+def test_place_bf16_integer_valued_exact(engine, P, N):
+    rng = np.random.default_rng(P + 3 * N)
+    WA, L, free, req = cluster(rng, P, N, dtype="bf16", lo=0, hi=16, cap_scale=0.05)
+    upload(engine, WA, L, free, req, "bf16")
+    node, cf, _ = engine.place()
+    want, wcost, wfree = oracle.place(WA, L, req, free, "bf16")
+    assert node.tolist() == want.tolist()
+    assert np.array_equal(cf.astype(np.float64), wcost)
+    assert (engine.get_capacity() == wfree).all()
+
+
+def test_cost_bf16_random_within_tolerance(engine):
+    """General bf16 operands, fp32 MFMA accumulation: candidate costs within
+    1e-5 relative of the fp64 oracle's cost for the same node, and each
+    candidate's fp64 cost within tolerance of the oracle's k-th best."""
+    rng = np.random.default_rng(5)
+    P, N = 512, 2048
+    WA, L, free, req = cluster(rng, P, N, dtype="bf16", int_valued=False, cap_scale=1.0)
+    upload(engine, WA, L, free, req, "bf16")
+    engine.score()
+    node, _, cf, cnt = engine.candidates()
+    cost = oracle.cost(WA, L, "bf16")
+    mask = oracle.fit_mask(req, free)
+    wn, wc, wcnt = oracle.topk(cost, mask, 4)
+    assert (cnt == wcnt).all()
+    rows = np.arange(P)[:, None]
+    exact = cost[rows, np.maximum(node, 0)]
+    rel = np.abs(cf.astype(np.float64) - exact) / np.abs(exact)
+    assert rel[node >= 0].max() <= REL_TOL
+    # the GPU's j-th candidate is a true j-th best up to the tolerance
+    assert (np.abs(exact - wc) <= REL_TOL * np.abs(wc))[node >= 0].all()
+
+
+def test_csr_traffic_matches_dense(engine):
+    rng = np.random.default_rng(8)
+    P, N = 600, 300
+    _, L, free, req = cluster(rng, P, N, cap_scale=0.2)
+    deg = rng.integers(0, 12, P)
+    row_ptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int32)
+    peer = rng.integers(-1, N, row_ptr[-1]).astype(np.int32)  # -1 = unbound peer
+    peer[rng.random(len(peer)) < 0.3] = rng.integers(0, 4, 1)[0]  # repeated nodes
+    w = rng.integers(1, 40, row_ptr[-1]).astype(np.int8)
+    dense = np.zeros((P, N), np.int32)
+    for p in range(P):
+        for x in range(row_ptr[p], row_ptr[p + 1]):
+            if peer[x] >= 0:
+                dense[p, peer[x]] += w[x]
+    dense = np.clip(dense, -128, 127).astype(np.int8)
+    engine.upload_latency(L, "i8")
+    engine.upload_capacity(free)
+    engine.upload_pods(req)
+    engine.upload_traffic_csr(row_ptr, peer, w, "i8", N)
+    node_csr, _, c_csr = engine.place()
+    want, wcost, _ = oracle.place(dense, L, req, free, "i8")
+    assert node_csr.tolist() == want.tolist() and c_csr.tolist() == wcost.tolist()
+
+
+def test_deterministic_repeat(engine):
+    rng = np.random.default_rng(12)
+    WA, L, free, req = cluster(rng, 1500, 900, cap_scale=0.03)
+    upload(engine, WA, L, free, req, "i8")
+    a, _, ca = engine.place()
+    engine.reset_capacity()
+    b, _, cb = engine.place()
+    assert (a == b).all() and (ca == cb).all()
+
+
+def test_synthetic_cluster_sampled(engine):
+    """The bench's device-generated cluster (scaled down): candidate lists of
+    sampled pods equal the oracle top-4 on the inputs read back from HBM, and
+    the commit equals the sequential oracle replayed on the GPU's lists."""
+    N, P = 2048, 8192
+    engine.synth_cluster(0x4E4153, N, P, "i8", peers=8)
+    engine.score()
+    node, ci, _, cnt = engine.candidates()
+    rng = np.random.default_rng(0)
+    pods = np.sort(rng.choice(P, 64, replace=False))
+    _, L, cap, req = engine.read_inputs(0, 0, want_L=True)
+    for p in pods:
+        WA, _, _, _ = engine.read_inputs(int(p), 1, want_L=False)
+        cost = oracle.cost(WA, L, "i8")
+        mask = oracle.fit_mask(req[p:p + 1], cap)
+        wn, wc, wcnt = oracle.topk(cost, mask, 4)
+        assert cnt[p] == wcnt[0] and (node[p] == wn[0]).all() and (ci[p][: cnt[p]] == wc[0][: cnt[p]]).all()
+    engine.reset_capacity()
+    placed, _, _ = engine.place()
+    want, _, wfree, stop = oracle.commit(node, cnt, req, cap)
+    assert stop == P  # no rescore needed on this workload
+    assert placed.tolist() == want.tolist()
+    assert (engine.get_capacity() == wfree).all()

@@ -1,0 +1,43 @@
+"""Seeded input generators shared by the CPU and GPU tests."""
+import itertools
+
+import numpy as np
+
+from golden.make_golden import random_snapshot  # noqa: F401  (re-export)
+
+
+def stack_snapshots(snaps):
+    return {k: np.stack([s[k] for s in snaps]) for k in snaps[0]}
+
+
+def f32_to_bf16_bits(x):
+    """Round-to-nearest-even float32 -> bf16 bits (finite inputs)."""
+    u = np.asarray(x, np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def bf16_bits_to_f64(b):
+    return (np.asarray(b, np.uint16).astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+
+
+def cluster(rng, P, N, dtype="i8", lo=0, hi=20, cap_scale=1.0, int_valued=True):
+    """Random extended-mode instance: WA (P,N), L (N,N), free (N,3), req (P,3)."""
+    if dtype == "i8":
+        WA = rng.integers(lo, hi, (P, N)).astype(np.int8)
+        L = rng.integers(lo, hi, (N, N)).astype(np.int8)
+    elif int_valued:
+        WA = f32_to_bf16_bits(rng.integers(lo, hi, (P, N)).astype(np.float32))
+        L = f32_to_bf16_bits(rng.integers(lo, hi, (N, N)).astype(np.float32))
+    else:
+        WA = f32_to_bf16_bits(rng.random((P, N)).astype(np.float32))
+        L = f32_to_bf16_bits((1.0 + 999.0 * rng.random((N, N))).astype(np.float32))
+    free = np.stack([rng.integers(int(2000 * cap_scale), int(8000 * cap_scale) + 1, N),
+                     rng.integers(int(2e6 * cap_scale), int(8e6 * cap_scale) + 1, N),
+                     np.full(N, max(1, int(110 * cap_scale)))], 1).astype(np.int32)
+    req = np.stack([rng.integers(1, 540, P), rng.integers(7_464, 303_749, P),
+                    np.ones(P, np.int64)], 1).astype(np.int32)
+    return WA, L, free, req
+
+
+def all_perms(n):
+    return np.array(list(itertools.permutations(range(n))), np.int32)
