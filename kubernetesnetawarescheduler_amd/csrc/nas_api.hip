@@ -170,6 +170,14 @@ int check_extended(nas_ctx *ctx) {
     if (!ctx->have_L || !ctx->have_cap || !ctx->have_pods || !ctx->have_wa)
         return nas::fail(ctx, NAS_ERR_STATE,
                          "nas_place needs latency, capacity, pods and traffic uploaded");
+    if (ctx->L_n != ctx->cap_n || ctx->L_n != ctx->wa_n)
+        return nas::fail(ctx, NAS_ERR_ARG, "node counts of latency / capacity / traffic differ");
+    if (ctx->req_P != ctx->wa_P)
+        return nas::fail(ctx, NAS_ERR_ARG, "pod counts of requests / traffic differ");
+    if (ctx->L_dtype != ctx->wa_dtype)
+        return nas::fail(ctx, NAS_ERR_ARG, "dtypes of latency / traffic differ");
+    if (ctx->N != ctx->L_n || ctx->P != ctx->req_P || ctx->dtype != ctx->L_dtype)
+        return nas::fail(ctx, NAS_ERR_STATE, "re-upload latency and traffic after resizing");
     return NAS_OK;
 }
 
@@ -375,11 +383,8 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
         return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_latency: L / n / dtype");
     if ((int64_t)n * 127 * 128 >= (int64_t)1 << 31 && dtype == NAS_DT_I8)
         return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "int8 path: n too large for exact int32 costs");
-    if ((ctx->have_cap || ctx->have_pods || ctx->have_wa) && (ctx->N != n))
-        return nas::fail(ctx, NAS_ERR_ARG, "node count differs from earlier uploads");
-    if (ctx->have_wa && ctx->dtype != dtype)
-        return nas::fail(ctx, NAS_ERR_ARG, "dtype differs from the uploaded traffic");
     set_geometry(ctx, n, dtype);
+    if (ctx->have_wa && (ctx->wa_n != n || ctx->wa_dtype != dtype)) ctx->have_wa = false;
     const size_t e = esz(dtype);
     OK(nas::ensure(ctx, ctx->Lt, (size_t)ctx->Mp * ctx->Kp * e));
     DevBuf tmp;
@@ -392,6 +397,8 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
     (void)hipFree(tmp.p);
     if (he != hipSuccess) return nas::hip_fail(ctx, he, "upload latency");
     ctx->have_L = true;
+    ctx->L_n = n;
+    ctx->L_dtype = dtype;
     ctx->synth_valid = false;
     return NAS_OK;
 }
@@ -401,8 +408,6 @@ int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *m
     OK(bind(ctx));
     if (!cpu_milli || !mem_kib || !pods || n <= 0)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_capacity");
-    if ((ctx->have_L || ctx->have_pods || ctx->have_wa) && ctx->N != n)
-        return nas::fail(ctx, NAS_ERR_ARG, "node count differs from earlier uploads");
     if (!ctx->have_L && !ctx->have_wa) set_geometry(ctx, n, ctx->dtype ? ctx->dtype : NAS_DT_I8);
     OK(nas::ensure(ctx, ctx->cap0, (size_t)3 * n * 4));
     OK(nas::ensure(ctx, ctx->cap, (size_t)3 * n * 4));
@@ -413,16 +418,16 @@ int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *m
     HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * n * 4, hipMemcpyDeviceToDevice,
                          ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
-    ctx->N = n;
     ctx->have_cap = true;
+    ctx->cap_n = n;
     return NAS_OK;
 }
 
 int nas_reset_capacity(nas_ctx *ctx) {
     OK(bind(ctx));
     if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
-    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * ctx->N * 4, hipMemcpyDeviceToDevice,
-                         ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * ctx->cap_n * 4,
+                         hipMemcpyDeviceToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
     return NAS_OK;
 }
@@ -431,7 +436,7 @@ int nas_get_capacity(nas_ctx *ctx, int32_t *cpu_milli, int32_t *mem_kib, int32_t
                      int32_t n) {
     OK(bind(ctx));
     if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
-    if (n != ctx->N || !cpu_milli || !mem_kib || !pods)
+    if (n != ctx->cap_n || !cpu_milli || !mem_kib || !pods)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_get_capacity");
     int32_t *dst[3] = {cpu_milli, mem_kib, pods};
     for (int r = 0; r < 3; ++r)
@@ -445,8 +450,6 @@ int nas_upload_pods(nas_ctx *ctx, const int32_t *rc, const int32_t *rm, const in
                     int32_t P) {
     OK(bind(ctx));
     if (!rc || !rm || !rp || P <= 0) return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_pods");
-    if (ctx->have_wa && ctx->P != P)
-        return nas::fail(ctx, NAS_ERR_ARG, "pod count differs from the uploaded traffic");
     for (int p = 0; p < P; ++p)
         if (rc[p] < 0 || rm[p] < 0 || rp[p] < 0)
             return nas::fail(ctx, NAS_ERR_ARG, "negative resource request");
@@ -458,8 +461,11 @@ int nas_upload_pods(nas_ctx *ctx, const int32_t *rc, const int32_t *rm, const in
     OK(nas::ensure(ctx, ctx->req, h.size() * 4));
     HIPCK(hipMemcpyAsync(ctx->req.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
-    ctx->P = P;
-    ctx->Pp = Pp;
+    if (!ctx->have_wa) {
+        ctx->P = P;
+        ctx->Pp = Pp;
+    }
+    ctx->req_P = P;
     ctx->have_pods = true;
     return NAS_OK;
 }
@@ -467,17 +473,17 @@ int nas_upload_pods(nas_ctx *ctx, const int32_t *rc, const int32_t *rm, const in
 static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
     if (P <= 0 || n <= 0 || (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
         return nas::fail(ctx, NAS_ERR_ARG, "traffic: P / n / dtype");
-    if ((ctx->have_L || ctx->have_cap) && ctx->N != n)
-        return nas::fail(ctx, NAS_ERR_ARG, "node count differs from earlier uploads");
-    if (ctx->have_L && ctx->dtype != dtype)
-        return nas::fail(ctx, NAS_ERR_ARG, "dtype differs from the uploaded latency");
-    if (ctx->have_pods && ctx->P != P)
-        return nas::fail(ctx, NAS_ERR_ARG, "pod count differs from the uploaded pods");
-    if (!ctx->have_L) set_geometry(ctx, n, dtype);
+    if (!ctx->have_L || ctx->L_n != n || ctx->L_dtype != dtype) {
+        set_geometry(ctx, n, dtype);
+        ctx->have_L = false;  // its layout no longer matches: re-upload latency
+    }
     ctx->P = P;
     ctx->Pp = (int32_t)nas::round_up(P, nas::COST_BN);
     OK(nas::ensure(ctx, ctx->WA, (size_t)ctx->Pp * ctx->Kp * esz(dtype)));
     HIPCK(hipMemsetAsync(ctx->WA.p, 0, (size_t)ctx->Pp * ctx->Kp * esz(dtype), ctx->stream));
+    ctx->wa_P = P;
+    ctx->wa_n = n;
+    ctx->wa_dtype = dtype;
     return NAS_OK;
 }
 
@@ -534,6 +540,8 @@ int nas_filter(nas_ctx *ctx, uint64_t *mask_out) {
     OK(bind(ctx));
     if (!ctx->have_cap || !ctx->have_pods || ctx->N <= 0)
         return nas::fail(ctx, NAS_ERR_STATE, "nas_filter needs capacity and pods");
+    if (ctx->cap_n != ctx->N || ctx->req_P != ctx->P)
+        return nas::fail(ctx, NAS_ERR_STATE, "nas_filter: capacity/pods do not match the geometry");
     OK(alloc_extended(ctx));
     Timer tm(ctx);
     hipEvent_t a = tm.mark();
@@ -743,6 +751,9 @@ int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, i
                          ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
     ctx->have_L = ctx->have_cap = ctx->have_pods = ctx->have_wa = true;
+    ctx->L_n = ctx->cap_n = ctx->wa_n = n_nodes;
+    ctx->req_P = ctx->wa_P = P;
+    ctx->L_dtype = ctx->wa_dtype = dtype;
     ctx->synth_valid = true;
     ctx->synth_seed = seed;
     return NAS_OK;

@@ -64,6 +64,7 @@ struct nas_ctx {
     int32_t Mp = 0;          // padded local node count (multiple of COST_BM)
     int32_t Pp = 0;          // padded pod count (multiple of COST_BN)
     bool have_L = false, have_cap = false, have_pods = false, have_wa = false;
+    int32_t L_n = 0, L_dtype = 0, cap_n = 0, req_P = 0, wa_P = 0, wa_n = 0, wa_dtype = 0;
     nas::DevBuf Lt;          // [Mp][Kp] elements: Lt[i][m] = L[m][Nloc0 + i]
     nas::DevBuf WA;          // [Pp][Kp] elements
     nas::DevBuf cap0, cap;   // [3][N] int32 (initial, working)
