@@ -46,43 +46,56 @@ k_commit(const unsigned long long *__restrict__ cand_key, const int *__restrict_
         return __hip_atomic_load(cap + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
 
+    // candidates + requests of 64 consecutive pods, one pod per lane;
+    // two chunks are prefetched ahead (the common advance is a full 64)
+    struct Chunk {
+        unsigned long long k[KC];
+        int r0, r1, r2;
+    };
+    auto load = [&](int base, Chunk &c) {
+        const int i = base + lane;
+        if (i < p_end) {
+            const ulonglong2 *s = reinterpret_cast<const ulonglong2 *>(cand_key + (size_t)i * KC);
+            const ulonglong2 x = s[0], y = s[1];
+            c.k[0] = x.x; c.k[1] = x.y; c.k[2] = y.x; c.k[3] = y.y;
+            c.r0 = req[i]; c.r1 = req[Pp + i]; c.r2 = req[2 * Pp + i];
+        } else {
+#pragma unroll
+            for (int j = 0; j < KC; ++j) c.k[j] = KEY_INVALID;
+            c.r0 = c.r1 = c.r2 = 0;
+        }
+    };
+
     int stop = p_end;
     int p = p_begin;
+    Chunk cur, nx1, nx2;
+    load(p, cur);
+    load(p + 64, nx1);
+    load(p + 128, nx2);
     while (p < p_end) {
         const int i = p + lane;
         const bool active = i < p_end;
-        unsigned long long k[KC];
-        int r0 = 0, r1 = 0, r2 = 0;
-        if (active) {
-            const ulonglong2 *s = reinterpret_cast<const ulonglong2 *>(cand_key + (size_t)i * KC);
-            const ulonglong2 x = s[0], y = s[1];
-            k[0] = x.x; k[1] = x.y; k[2] = y.x; k[3] = y.y;
-            r0 = req[i]; r1 = req[Pp + i]; r2 = req[2 * Pp + i];
-        } else {
-#pragma unroll
-            for (int j = 0; j < KC; ++j) k[j] = KEY_INVALID;
-        }
         int choice = -1, nvalid = 0;
         unsigned ccost = 0;
 #pragma unroll
         for (int j = 0; j < KC; ++j) {
-            if (k[j] != KEY_INVALID) {
+            if (cur.k[j] != KEY_INVALID) {
                 ++nvalid;
                 if (choice < 0) {
-                    const int n = (int)(unsigned)k[j];
-                    if (r0 <= ld(n) && r1 <= ld(N + n) && r2 <= ld(2 * N + n)) {
+                    const int n = (int)(unsigned)cur.k[j];
+                    if (cur.r0 <= ld(n) && cur.r1 <= ld(N + n) && cur.r2 <= ld(2 * N + n)) {
                         choice = n;
-                        ccost = (unsigned)(k[j] >> 32);
+                        ccost = (unsigned)(cur.k[j] >> 32);
                     }
                 }
             }
         }
         const bool rescore = active && choice < 0 && nvalid == KC;
+        // repeated picks inside the chunk: the lowest lane per bucket wins
+        // (one wave: LDS operations complete in issue order, no barrier)
         const int h = choice & (HBUCKETS - 1);
         if (choice >= 0) atomicMin(&table[h], lane);
-        __syncthreads();
         const bool dup = choice >= 0 && table[h] != lane;
-        __syncthreads();
         if (choice >= 0) table[h] = FREE_SLOT;
         const unsigned long long bad = __ballot(rescore || dup);
         const int f = bad ? __ffsll((long long)bad) - 1 : 64;
@@ -90,21 +103,29 @@ k_commit(const unsigned long long *__restrict__ cand_key, const int *__restrict_
             if (choice >= 0) {
                 // picks of lanes < f are pairwise distinct: plain updates
                 if (LDS_CAP) {
-                    cap[choice] -= r0; cap[N + choice] -= r1; cap[2 * N + choice] -= r2;
+                    cap[choice] -= cur.r0; cap[N + choice] -= cur.r1; cap[2 * N + choice] -= cur.r2;
                 } else {
-                    atomicSub(cap + choice, r0); atomicSub(cap + N + choice, r1);
-                    atomicSub(cap + 2 * N + choice, r2);
+                    atomicSub(cap + choice, cur.r0); atomicSub(cap + N + choice, cur.r1);
+                    atomicSub(cap + 2 * N + choice, cur.r2);
                 }
             }
             out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
             out_cost[i] = ccost;
         }
-        __syncthreads();
         if (f < 64 && ((__ballot(rescore) >> f) & 1ull)) {
             stop = p + f;
             break;
         }
         p += f;
+        if (f == 64) {
+            cur = nx1;
+            nx1 = nx2;
+            load(p + 128, nx2);
+        } else {
+            load(p, cur);
+            load(p + 64, nx1);
+            load(p + 128, nx2);
+        }
     }
     __syncthreads();
     if (LDS_CAP)

@@ -40,9 +40,9 @@ typedef unsigned long long u64;
 constexpr int THREADS = 512;
 constexpr int BM = COST_BM;   // nodes per tile
 constexpr int BN = COST_BN;   // pods per tile
-constexpr int BKB = COST_BKB; // bytes of K per stage
+constexpr int BKB = COST_BKB; // bytes of K per LDS stage (full 128-byte lines)
 constexpr int STAGE_BYTES = (BM + BN) * BKB;  // 64 KiB
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;    // 128 KiB
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;    // 128 KiB, double-buffered
 constexpr int GM = 4;  // node tiles per L2 group
 
 template <int DT>
@@ -87,6 +87,28 @@ __device__ __forceinline__ void insert4(u64 (&k)[4], u64 x) {
     t = umin(k[0], k[1]); k[1] = umax(k[0], k[1]); k[0] = t;
 }
 
+// Per-lane running top-4 as separate (orderable cost, node) u32 words.
+// A lane visits its nodes in ascending node order, so a new (x, n) sorts
+// before entry j iff x < cost[j] strictly (an equal cost has the larger node):
+// four independent 32-bit compares and a select network, no 64-bit compares.
+struct Top4 {
+    unsigned c[4], n[4];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = n[j] = 0xffffffffu;
+    }
+    __device__ __forceinline__ void insert(unsigned x, unsigned node) {
+        const bool b0 = x < c[0], b1 = x < c[1], b2 = x < c[2], b3 = x < c[3];
+        const unsigned c3 = b2 ? c[2] : (b3 ? x : c[3]), n3 = b2 ? n[2] : (b3 ? node : n[3]);
+        const unsigned c2 = b1 ? c[1] : (b2 ? x : c[2]), n2 = b1 ? n[1] : (b2 ? node : n[2]);
+        const unsigned c1 = b0 ? c[0] : (b1 ? x : c[1]), n1 = b0 ? n[0] : (b1 ? node : n[1]);
+        c[0] = b0 ? x : c[0];
+        n[0] = b0 ? node : n[0];
+        c[1] = c1; n[1] = n1; c[2] = c2; n[2] = n2; c[3] = c3; n[3] = n3;
+    }
+    __device__ __forceinline__ u64 key(int j) const { return ((u64)c[j] << 32) | n[j]; }
+};
+
 // top-4 of two sorted 4-lists (bitonic: min against the reversed list, then a
 // 4-element bitonic merge)
 __device__ __forceinline__ void merge4(u64 (&a)[4], const u64 (&b)[4]) {
@@ -105,7 +127,10 @@ __device__ __forceinline__ u64 shfl_xor64(u64 x, int m) {
     return ((u64)(unsigned)hi << 32) | (unsigned)lo;
 }
 
-template <int DT>
+// EPI != 0 are diagnostic variants for tools/mb_cost.hip: 1 = accumulators
+// kept alive with an empty asm and no epilogue (times the main loop alone),
+// 2 = per-lane top-1 instead of top-4.
+template <int DT, int EPI = 0>
 __global__ void __launch_bounds__(THREADS, 1)
 k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
@@ -132,8 +157,11 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
     const unsigned char *Bg = WA + (size_t)(p0 + nt * BN) * Kb;
 
-    // LDS-DMA staging: instruction j of wave w fills rows (8j + w)*8 .. +8 of
-    // A and of B (1 KiB each, lane-linear); the chunk swizzle is on the source.
+    // LDS-DMA staging: piece j of wave w fills rows (8j + w)*8 .. +8 of A
+    // and of B (1 KiB each, lane-linear: lane l -> row + l/8, 16-byte chunk
+    // l%8; whole 128-byte lines per row -- 64-byte row pieces measured 12%
+    // slower); the chunk swizzle chunk ^= (row >> 1) & 7 is applied on the
+    // SOURCE address so fragment reads are bank-conflict free.
     const int srow_in = lane >> 3;
     const int sq = lane & 7;
     auto stage = [&](int buf, int k0) {
@@ -160,7 +188,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         const unsigned char *As = lds + buf * STAGE_BYTES;
         const unsigned char *Bs = As + BM * BKB;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
+        for (int kk = 0; kk < BKB / 32; ++kk) {
             const int c = kk * 2 + fh;
             v4i a[4], bb[2];
 #pragma unroll
@@ -180,6 +208,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         }
     };
 
+    // two-stage pipeline: stage t+1 streams in (LDS-DMA) while stage t is read
     const int nk = Kb / BKB;
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -192,12 +221,24 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         __syncthreads();
     }
 
+    if constexpr (EPI == 1) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                asm volatile("" ::"v"(acc[mi][ni]));
+#endif
+            }
+        return;
+    }
     // ---- epilogue: fit mask + per-pod top-4
     u64 key[2][4];
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) key[ni][j] = KEY_INVALID;
+        Top4 t4;
+        t4.init();
+        unsigned best1 = 0xffffffffu, bnode1 = 0xffffffffu;
         const int pod = p0 + nt * BN + wn * 64 + ni * 32 + fr;
 #pragma unroll
         for (int mi2 = 0; mi2 < 2; ++mi2) {
@@ -211,13 +252,21 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 #pragma unroll
                 for (int reg = 0; reg < 16; ++reg) {
                     const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
-                    const u64 k = ((bits >> row) & 1u)
-                                      ? ((u64)M::okey(acc[mi][ni][reg]) << 32) | (node0 + row)
-                                      : KEY_INVALID;
-                    insert4(key[ni], k);
+                    // not fitting -> cost all-ones, never inserted (branch-free)
+                    const unsigned x = M::okey(acc[mi][ni][reg]) | ((((bits >> row) & 1u) ^ 1u) * 0xffffffffu);
+                    if constexpr (EPI == 2) {
+                        const bool b = x < best1;
+                        best1 = b ? x : best1;
+                        bnode1 = b ? node0 + row : bnode1;
+                    } else {
+                        t4.insert(x, node0 + row);
+                    }
                 }
             }
         }
+        if constexpr (EPI == 2) t4.c[0] = best1, t4.n[0] = bnode1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) key[ni][j] = t4.c[j] == 0xffffffffu ? KEY_INVALID : t4.key(j);
         // lanes l and l^32 hold the same pod, complementary node rows
         u64 o[4];
 #pragma unroll
@@ -287,6 +336,13 @@ __global__ void k_unpack(const u64 *__restrict__ keys, int p0, int np, int *__re
     }
     cnt[p] = c;
 }
+
+#ifdef NAS_DIAG_VARIANTS
+template __global__ void k_cost_topk<NAS_DT_I8, 1>(const unsigned char *, const unsigned char *, int,
+                                                   int, int, int, int, const u64 *, u64 *, int);
+template __global__ void k_cost_topk<NAS_DT_I8, 2>(const unsigned char *, const unsigned char *, int,
+                                                   int, int, int, int, const u64 *, u64 *, int);
+#endif
 
 template <int DT>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,

@@ -7,9 +7,9 @@
 //
 // Layout: lane-per-node.  Each wave owns a 64-node chunk and keeps that
 // chunk's free capacity in VGPRs (one coalesced SoA read); it then walks the
-// pods, whose requests are wave-uniform scalar loads, and the three vector
-// compares produce the 64-bit fit mask of (pod, chunk) directly in an SGPR
-// pair (a ballot).  64 consecutive pods' masks are collected one per lane and
+// pods 64 at a time: one coalesced load of their requests, broadcast to the
+// wave with v_readlane, and the three vector compares produce the 64-bit fit
+// mask of (pod, chunk) directly in an SGPR pair (a ballot).  64 consecutive pods' masks are collected one per lane and
 // written with one coalesced 8-byte-per-lane store:
 //   mask[c * Pp + p]  bit j  <=>  pod p fits local node 64c + j.
 // HBM-bound on the mask write (P*N/8 bytes) -- see DESIGN.md.
@@ -39,15 +39,21 @@ k_fit(const int *__restrict__ cap, int N, int n0, int nloc, int n_chunks,
     const int pb = p0 + blockIdx.x * FIT_PODS_PER_BLOCK;
     const int pe = min(p_end, pb + FIT_PODS_PER_BLOCK);
     for (int p = pb; p < pe; p += 64) {
+        // one coalesced load of 64 pods' requests, broadcast with v_readlane
+        const int q = p + lane;
+        const int a = q < pe ? rc[q] : 0x7fffffff;
+        const int b = q < pe ? rm[q] : 0x7fffffff;
+        const int d = q < pe ? rp[q] : 0x7fffffff;
         unsigned long long mine = 0;
-        const int cnt = min(64, pe - p);
-#pragma unroll 8
-        for (int i = 0; i < cnt; ++i) {
-            const int q = p + i;  // wave-uniform -> scalar loads
-            const unsigned long long m = __ballot(rc[q] <= fc && rm[q] <= fm && rp[q] <= fp);
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            const int ra = __builtin_amdgcn_readlane(a, i);
+            const int rb = __builtin_amdgcn_readlane(b, i);
+            const int rd = __builtin_amdgcn_readlane(d, i);
+            const unsigned long long m = __ballot(ra <= fc && rb <= fm && rd <= fp);
             mine = lane == i ? m : mine;
         }
-        if (lane < cnt) mask[(size_t)c * Pp + p + lane] = mine;
+        if (q < pe) mask[(size_t)c * Pp + q] = mine;
     }
 }
 

@@ -129,6 +129,8 @@ __global__ void k_synth_snap(unsigned long long seed, int n, long long ns, int S
 // Extended-mode cluster (build-defined):
 // nodes in racks of 32, racks in zones of 16; symmetric latency by distance
 // class (0 self, 2-4 same rack, 12-19 same zone, 40-105 cross zone);
+// traffic: dense background 0..2 to every node plus `peers` heavy bound peers
+// (16..127) in the pod's home rack / zone, saturated at 127;
 // capacity cpu {4000, 8000} m, memory {4, 8} GiB, 110 pods; requests
 // log-uniform over the clusterloader2 ranges (cpu 0.000213-0.5376 cores, mem
 // 7.6-311 MB, datasets/clusterloader2/*/*.json), 1 pod slot.
@@ -148,6 +150,29 @@ __device__ __forceinline__ signed char from_int<signed char>(int v) { return (si
 template <>
 __device__ __forceinline__ unsigned short from_int<unsigned short>(int v) {
     return (unsigned short)(__float_as_uint((float)v) >> 16);  // exact for |v| <= 256
+}
+
+template <typename T>
+__device__ __forceinline__ int to_int(T v);
+template <>
+__device__ __forceinline__ int to_int<signed char>(signed char v) { return v; }
+template <>
+__device__ __forceinline__ int to_int<unsigned short>(unsigned short v) {
+    return (int)__uint_as_float((unsigned)v << 16);
+}
+
+// dense background traffic 0..2 to every node (every pod talks a little to
+// everything: the contraction is genuinely dense), zero padding past N
+template <typename T>
+__global__ void k_synth_bg(unsigned long long seed, int N, int P, int Kp, long long total,
+                           T *__restrict__ WA) {
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int p = (int)(t / Kp), m = (int)(t - (long long)p * Kp);
+        int v = 0;
+        if (p < P && m < N) v = (int)(mix64(seed ^ ((unsigned long long)t * 0x9e3779b97f4a7c15ull)) % 3);
+        WA[t] = from_int<T>(v);
+    }
 }
 
 template <typename T>
@@ -171,7 +196,8 @@ __global__ void k_synth_lfull(unsigned long long seed, int N, T *__restrict__ L)
     }
 }
 
-// one thread per pod: peers in the home rack (all but 2) and in the zone
+// one thread per pod: heavy peers in the home rack (all but 2) and in the
+// zone, added on top of the background
 template <typename T>
 __global__ void k_synth_pods(unsigned long long seed, int N, int P, int peers, int Kp, int Pp,
                              T *__restrict__ WA, int *__restrict__ req) {
@@ -200,7 +226,7 @@ __global__ void k_synth_pods(unsigned long long seed, int N, int P, int peers, i
         bool seen = false;
         for (int y = 0; y < j; ++y) seen |= nodes[y] == nodes[j];
         if (seen) continue;
-        int s = 0;
+        int s = to_int<T>(WA[(size_t)p * Kp + nodes[j]]);  // background
         for (int y = j; y < np; ++y) s += nodes[y] == nodes[j] ? wts[y] : 0;
         WA[(size_t)p * Kp + nodes[j]] = from_int<T>(min(s, 127));
     }
@@ -269,7 +295,6 @@ hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int64_t 
 hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
                                 int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
                                 int32_t *cap, int32_t *req, void *L_full) {
-    const size_t esz = dtype == NAS_DT_I8 ? 1 : 2;
     hipError_t e;
     if (Lt) {
         if (dtype == NAS_DT_I8)
@@ -290,7 +315,14 @@ hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (WA) {
-        if ((e = hipMemsetAsync(WA, 0, (size_t)Pp * Kp * esz, st)) != hipSuccess) return e;
+        const long long tot = (long long)Pp * Kp;
+        if (dtype == NAS_DT_I8)
+            k_synth_bg<signed char><<<grid_for(tot, 256), 256, 0, st>>>(
+                seed, N, P, Kp, tot, static_cast<signed char *>(WA));
+        else
+            k_synth_bg<unsigned short><<<grid_for(tot, 256), 256, 0, st>>>(
+                seed, N, P, Kp, tot, static_cast<unsigned short *>(WA));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
         if (dtype == NAS_DT_I8)
             k_synth_pods<signed char><<<(Pp + 255) / 256, 256, 0, st>>>(
                 seed, N, P, peers, Kp, Pp, static_cast<signed char *>(WA), req);
