@@ -62,8 +62,10 @@ extern "C" {
 #define NAS_W_BANDWIDTH 4 /* always NAS_NONE: the :353 bug */
 #define NAS_W_DISK 5
 
-/* number of candidates kept per pod between scoring and commit */
-#define NAS_K_CANDIDATES 4
+/* candidates kept per pod between scoring and commit: the 8 smallest
+ * (cost, node) among fitting nodes, of which the first `count` are
+ * guaranteed to be the exact global ranking (see nas_get_candidates) */
+#define NAS_K_CANDIDATES 8
 
 typedef struct nas_ctx nas_ctx;
 
@@ -178,11 +180,14 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
 int nas_score(nas_ctx *ctx);
 
 /* Candidate lists of the last scoring pass (nas_score, or nas_place after
- * its rescore rounds): cand_node[P*K] (sorted by (cost, node); -1 past
- * count), cand_cost_i[P*K] exact int cost (NAS_DT_I8), cand_cost_f[P*K]
- * cost as float, count[P].  Any output may be NULL. */
+ * its rescore rounds): cand_node[P*K] sorted by (cost, node), -1 past
+ * count; count[P] = number of leading entries that are exactly the pod's
+ * best fitting nodes in order (at least min(4, #fitting nodes); entries past
+ * count are not returned); cand_cost_i[P*K] exact int cost (NAS_DT_I8),
+ * cand_cost_f[P*K] cost as float; complete[P] = 1 iff the list holds every
+ * node that fit when it was scored.  Any output may be NULL. */
 int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i,
-                       float *cand_cost_f, int32_t *count);
+                       float *cand_cost_f, int32_t *count, int32_t *complete);
 
 /* ---- multi-GPU: node axis sharded over the GPUs of one node ---------------
  * Rank r of `world` owns node columns [r*n/world, (r+1)*n/world) of L; pods,

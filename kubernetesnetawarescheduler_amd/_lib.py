@@ -22,7 +22,7 @@ NAS_NONE = -2
 NAS_EMPTY = -1
 NAS_DT_I8 = 1
 NAS_DT_BF16 = 2
-K_CANDIDATES = 4
+K_CANDIDATES = 8
 
 _ERRNAMES = {
     NAS_ERR_ARG: "NAS_ERR_ARG", NAS_ERR_HIP: "NAS_ERR_HIP", NAS_ERR_STATE: "NAS_ERR_STATE",
@@ -78,7 +78,7 @@ SIGNATURES = {
     "nas_filter": (_I, [_CTX, _V]),
     "nas_score": (_I, [_CTX]),
     "nas_place": (_I, [_CTX, _V, _V, _V]),
-    "nas_get_candidates": (_I, [_CTX, _V, _V, _V, _V]),
+    "nas_get_candidates": (_I, [_CTX, _V, _V, _V, _V, _V]),
     "nas_comm_unique_id": (_I, [_V]),
     "nas_comm_init": (_I, [_CTX, _V, _I, _I]),
     "nas_synth_snapshots": (_I, [_CTX, _c.c_uint64, _I, _I]),

@@ -23,10 +23,11 @@
 // (pod tiles) super-tile.
 //
 // Epilogue: per lane, 64 (node, cost) values per pod -> mask from the fit
-// kernel (bit per node) -> packed key (orderable cost << 32 | node) -> sorted
-// top-4 in registers -> merge with lane^32 -> merge across the two node-half
-// waves through LDS -> partial[node_tile][pod][4] (32 B per pod per tile).
-#include "nas_internal.h"
+// kernel (bit per node) -> sorted top-4 of (orderable cost, node) in
+// registers -> merged with lane^32 into an 8-list with an exactness bound
+// (klist.h) -> merged across the two node-half waves through LDS ->
+// partial[node_tile][pod][8] + pbound[node_tile][pod] (72 B per pod per tile).
+#include "klist.h"
 
 namespace nas {
 namespace {
@@ -35,7 +36,6 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned long long u64;
 
 constexpr int THREADS = 512;
 constexpr int BM = COST_BM;   // nodes per tile
@@ -76,17 +76,6 @@ __device__ __forceinline__ void glds16(const void *g, void *l) {
                                      (void __attribute__((address_space(3))) *)l, 16, 0, 0);
 }
 
-__device__ __forceinline__ u64 umin(u64 a, u64 b) { return a < b ? a : b; }
-__device__ __forceinline__ u64 umax(u64 a, u64 b) { return a < b ? b : a; }
-
-// sorted 4-list insert (k0 <= k1 <= k2 <= k3)
-__device__ __forceinline__ void insert4(u64 (&k)[4], u64 x) {
-    k[3] = umin(k[3], x);
-    u64 t = umin(k[2], k[3]); k[3] = umax(k[2], k[3]); k[2] = t;
-    t = umin(k[1], k[2]); k[2] = umax(k[1], k[2]); k[1] = t;
-    t = umin(k[0], k[1]); k[1] = umax(k[0], k[1]); k[0] = t;
-}
-
 // Per-lane running top-4 as separate (orderable cost, node) u32 words.
 // A lane visits its nodes in ascending node order, so a new (x, n) sorts
 // before entry j iff x < cost[j] strictly (an equal cost has the larger node):
@@ -109,24 +98,6 @@ struct Top4 {
     __device__ __forceinline__ u64 key(int j) const { return ((u64)c[j] << 32) | n[j]; }
 };
 
-// top-4 of two sorted 4-lists (bitonic: min against the reversed list, then a
-// 4-element bitonic merge)
-__device__ __forceinline__ void merge4(u64 (&a)[4], const u64 (&b)[4]) {
-    u64 m0 = umin(a[0], b[3]), m1 = umin(a[1], b[2]), m2 = umin(a[2], b[1]), m3 = umin(a[3], b[0]);
-    u64 t;
-    t = umin(m0, m2); m2 = umax(m0, m2); m0 = t;
-    t = umin(m1, m3); m3 = umax(m1, m3); m1 = t;
-    t = umin(m0, m1); m1 = umax(m0, m1); m0 = t;
-    t = umin(m2, m3); m3 = umax(m2, m3); m2 = t;
-    a[0] = m0; a[1] = m1; a[2] = m2; a[3] = m3;
-}
-
-__device__ __forceinline__ u64 shfl_xor64(u64 x, int m) {
-    const int lo = __shfl_xor((int)(unsigned)x, m);
-    const int hi = __shfl_xor((int)(unsigned)(x >> 32), m);
-    return ((u64)(unsigned)hi << 32) | (unsigned)lo;
-}
-
 // EPI != 0 are diagnostic variants for tools/mb_cost.hip: 1 = accumulators
 // kept alive with an empty asm and no epilogue (times the main loop alone),
 // 2 = per-lane top-1 instead of top-4.
@@ -134,7 +105,7 @@ template <int DT, int EPI = 0>
 __global__ void __launch_bounds__(THREADS, 1)
 k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
-            u64 *__restrict__ partial, int node_base) {
+            u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base) {
     using M = Mma<DT>;
     using acc_t = typename M::acc_t;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -232,8 +203,11 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             }
         return;
     }
-    // ---- epilogue: fit mask + per-pod top-4
-    u64 key[2][4];
+    // ---- epilogue: fit mask + per-pod candidate list
+    // per lane: top-4 of its 64 (node, cost) values per pod; lanes l and l^32
+    // (same pod, complementary rows) merge into a sorted 8-list whose bound is
+    // the smaller of the two 4th keys (every key <= bound is in the list)
+    u64 key[2][8], bnd[2];
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
         Top4 t4;
@@ -265,88 +239,81 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             }
         }
         if constexpr (EPI == 2) t4.c[0] = best1, t4.n[0] = bnode1;
+        u64 k4[4], o4[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) key[ni][j] = t4.c[j] == 0xffffffffu ? KEY_INVALID : t4.key(j);
-        // lanes l and l^32 hold the same pod, complementary node rows
-        u64 o[4];
+        for (int j = 0; j < 4; ++j) k4[j] = t4.c[j] == 0xffffffffu ? KEY_INVALID : t4.key(j);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = shfl_xor64(key[ni][j], 32);
-        merge4(key[ni], o);
+        for (int j = 0; j < 4; ++j) o4[j] = shfl_xor64(k4[j], 32);
+        merge44(k4, o4, key[ni]);
+        bnd[ni] = umin64(k4[3], o4[3]);
     }
 
     // merge the two node-half waves (wm = 0, 1) through LDS
-    u64 *xk = reinterpret_cast<u64 *>(lds);  // [wn][ni][32][4], staging is dead
+    u64 *xk = reinterpret_cast<u64 *>(lds);  // [wn][ni][32][9], staging is dead
     if (wm == 1 && fh == 0) {
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
+        for (int ni = 0; ni < 2; ++ni) {
+            u64 *d = xk + ((wn * 2 + ni) * 32 + fr) * 9;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) xk[((wn * 2 + ni) * 32 + fr) * 4 + j] = key[ni][j];
+            for (int j = 0; j < 8; ++j) d[j] = key[ni][j];
+            d[8] = bnd[ni];
+        }
     }
     __syncthreads();
     if (wm == 0) {
-        const int ni = fh;  // lane < 32 -> pods wn*64 + 0..31, lane >= 32 -> +32..63
-        u64 mine[4], other[4];
+        // lane < 32 -> pods wn*64 + 0..31 (ni = 0), lane >= 32 -> +32..63 (ni = 1);
+        // two constant-index branches, not key[fh][j] (a runtime index puts
+        // the lists in scratch)
+        auto finish = [&](u64 (&mine)[8], u64 b, int ni) {
+            u64 other[8];
+            const u64 *s = xk + ((wn * 2 + ni) * 32 + fr) * 9;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            mine[j] = ni ? key[1][j] : key[0][j];
-            other[j] = xk[((wn * 2 + ni) * 32 + fr) * 4 + j];
-        }
-        merge4(mine, other);
-        const int pod = p0 + nt * BN + wn * 64 + lane;
-        u64 *dst = partial + ((size_t)mt * Pp + pod) * KC;
-        *reinterpret_cast<ulonglong2 *>(dst) = make_ulonglong2(mine[0], mine[1]);
-        *reinterpret_cast<ulonglong2 *>(dst + 2) = make_ulonglong2(mine[2], mine[3]);
+            for (int j = 0; j < 8; ++j) other[j] = s[j];
+            merge88(mine, other);
+            b = umin64(umin64(b, s[8]), mine[7]);
+            const int pod = p0 + nt * BN + wn * 64 + lane;
+            store8(partial + ((size_t)mt * Pp + pod) * KC, mine);
+            pbound[(size_t)mt * Pp + pod] = b;
+        };
+        if (fh == 0) finish(key[0], bnd[0], 0);
+        else finish(key[1], bnd[1], 1);
     }
 }
 
-// merge n_lists sorted 4-lists per pod: src[l * stride + p * 4 + j]
-__global__ void k_merge(const u64 *__restrict__ src, int n_lists, long long stride, int src_p0,
-                        int p0, int np, u64 *__restrict__ dst) {
+// merge n_lists candidate lists per pod (list l of pod p at
+// keys[l * stride + (p - src_p0) * KC], bound[l * bstride + p - src_p0])
+__global__ void k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_lists,
+                        long long stride, long long bstride, int src_p0, int p0, int np,
+                        u64 *__restrict__ dst, u64 *__restrict__ dst_bound) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= np) return;
     const int p = p0 + i;
-    const size_t ps = (size_t)(p - src_p0) * KC;
-    u64 a[4], bb[4];
-    const ulonglong2 *s = reinterpret_cast<const ulonglong2 *>(src + ps);
-    ulonglong2 x = s[0], y = s[1];
-    a[0] = x.x; a[1] = x.y; a[2] = y.x; a[3] = y.y;
+    const size_t ps = (size_t)(p - src_p0);
+    u64 a[8], bb[8];
+    load8(keys + ps * KC, a);
+    u64 bound = bounds[ps];
     for (int l = 1; l < n_lists; ++l) {
-        const ulonglong2 *t = reinterpret_cast<const ulonglong2 *>(src + l * stride + ps);
-        x = t[0]; y = t[1];
-        bb[0] = x.x; bb[1] = x.y; bb[2] = y.x; bb[3] = y.y;
-        merge4(a, bb);
+        load8(keys + l * stride + ps * KC, bb);
+        merge88(a, bb);
+        bound = umin64(umin64(bound, bounds[l * bstride + ps]), a[7]);
     }
-    ulonglong2 *d = reinterpret_cast<ulonglong2 *>(dst + (size_t)p * KC);
-    d[0] = make_ulonglong2(a[0], a[1]);
-    d[1] = make_ulonglong2(a[2], a[3]);
-}
-
-__global__ void k_unpack(const u64 *__restrict__ keys, int p0, int np, int *__restrict__ node,
-                         int *__restrict__ cnt) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= np) return;
-    const int p = p0 + i;
-    int c = 0;
-#pragma unroll
-    for (int j = 0; j < KC; ++j) {
-        const u64 k = keys[(size_t)p * KC + j];
-        const bool ok = k != KEY_INVALID;
-        node[(size_t)p * KC + j] = ok ? (int)(unsigned)k : -1;
-        c += ok;
-    }
-    cnt[p] = c;
+    store8(dst + (size_t)p * KC, a);
+    dst_bound[p] = bound;
 }
 
 #ifdef NAS_DIAG_VARIANTS
 template __global__ void k_cost_topk<NAS_DT_I8, 1>(const unsigned char *, const unsigned char *, int,
-                                                   int, int, int, int, const u64 *, u64 *, int);
+                                                   int, int, int, int, const u64 *, u64 *, u64 *,
+                                                   int);
 template __global__ void k_cost_topk<NAS_DT_I8, 2>(const unsigned char *, const unsigned char *, int,
-                                                   int, int, int, int, const u64 *, u64 *, int);
+                                                   int, int, int, int, const u64 *, u64 *, u64 *,
+                                                   int);
 #endif
 
 template <int DT>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,
-                         int p0, int np, const uint64_t *mask, uint64_t *partial, int node_base) {
+                         int p0, int np, const uint64_t *mask, uint64_t *partial,
+                         uint64_t *pbound, int node_base) {
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_cost_topk<DT>),
@@ -358,7 +325,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     k_cost_topk<DT><<<n_mt * n_nt, THREADS, LDS_BYTES, st>>>(
         static_cast<const unsigned char *>(Lt), static_cast<const unsigned char *>(WA), Kb, n_mt,
         n_nt, p0, Pp, reinterpret_cast<const u64 *>(mask), reinterpret_cast<u64 *>(partial),
-        node_base);
+        reinterpret_cast<u64 *>(pbound), node_base);
     return hipGetLastError();
 }
 
@@ -368,32 +335,27 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
 // p0 + np <= Pp; Mp multiple of BM.
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
-                            uint64_t *partial, int node_base) {
+                            uint64_t *partial, uint64_t *pbound, int node_base) {
     if (np <= 0) return hipSuccess;
     if (Mp % BM || np % BN || p0 + np > Pp) return hipErrorInvalidValue;
     if (dtype == NAS_DT_I8) {
         if (Kp % BKB) return hipErrorInvalidValue;
-        return launch_cost_t<NAS_DT_I8>(st, Lt, WA, Mp, Kp, Pp, p0, np, mask, partial, node_base);
+        return launch_cost_t<NAS_DT_I8>(st, Lt, WA, Mp, Kp, Pp, p0, np, mask, partial, pbound,
+                                        node_base);
     }
     if ((2 * Kp) % BKB) return hipErrorInvalidValue;
-    return launch_cost_t<NAS_DT_BF16>(st, Lt, WA, Mp, 2 * Kp, Pp, p0, np, mask, partial, node_base);
+    return launch_cost_t<NAS_DT_BF16>(st, Lt, WA, Mp, 2 * Kp, Pp, p0, np, mask, partial, pbound,
+                                      node_base);
 }
 
-hipError_t launch_merge(hipStream_t st, const uint64_t *partial, int n_lists, int64_t list_stride,
-                        int src_p0, int p0, int np, uint64_t *cand_key) {
+hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
+                        int64_t stride, int64_t bstride, int src_p0, int p0, int np,
+                        uint64_t *cand_key, uint64_t *cand_bound) {
     if (np <= 0) return hipSuccess;
-    k_merge<<<(np + 255) / 256, 256, 0, st>>>(reinterpret_cast<const u64 *>(partial), n_lists,
-                                                list_stride, src_p0, p0, np,
-                                                reinterpret_cast<u64 *>(cand_key));
-    return hipGetLastError();
-}
-
-hipError_t launch_unpack(hipStream_t st, const uint64_t *cand_key, int p0, int np, int dtype,
-                         int32_t *cand_node, int32_t *cand_cnt) {
-    (void)dtype;
-    if (np <= 0) return hipSuccess;
-    k_unpack<<<(np + 255) / 256, 256, 0, st>>>(reinterpret_cast<const u64 *>(cand_key), p0, np,
-                                                 cand_node, cand_cnt);
+    k_merge<<<(np + 255) / 256, 256, 0, st>>>(
+        reinterpret_cast<const u64 *>(keys), reinterpret_cast<const u64 *>(bounds), n_lists, stride,
+        bstride, src_p0, p0, np, reinterpret_cast<u64 *>(cand_key),
+        reinterpret_cast<u64 *>(cand_bound));
     return hipGetLastError();
 }
 

@@ -60,7 +60,7 @@ int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes) {
 
 namespace {
 
-constexpr int RESCORE_PODS = 4096;  // pods rescored per commit stop (multiple of COST_BN)
+constexpr int RESCORE_PODS = 1024;  // pods rescored per commit stop (multiple of COST_BN)
 
 int bind(nas_ctx *ctx) {
     if (!ctx) return NAS_ERR_ARG;
@@ -193,21 +193,30 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi) {
                           ctx->req.as<int32_t>(), ctx->P, ctx->Pp, p_lo, p_hi - p_lo, mask));
     hipEvent_t e1 = tm.mark();
     HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, ctx->Pp,
-                                pr0, np, mask, ctx->partial.as<uint64_t>(), ctx->Nloc0));
+                                pr0, np, mask, ctx->partial.as<uint64_t>(),
+                                ctx->pbound.as<uint64_t>(), ctx->Nloc0));
     hipEvent_t e2 = tm.mark();
     const int n_lists = ctx->Mp / nas::COST_BM;
-    HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), n_lists, (int64_t)ctx->Pp * KC, 0,
-                            p_lo, p_hi - p_lo, ctx->cand_key.as<uint64_t>()));
+    HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
+                            (int64_t)ctx->Pp * KC, ctx->Pp, 0, p_lo, p_hi - p_lo,
+                            ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>()));
     if (ctx->world > 1) {
-        // exchange the per-shard top-4 of pods [pr0, pr1) and merge across ranks
-        const size_t cnt = (size_t)np * KC;
-        ncclResult_t r = ncclAllGather(ctx->cand_key.as<uint64_t>() + (size_t)pr0 * KC,
-                                       ctx->gather.as<uint64_t>(), cnt, ncclUint64,
-                                       reinterpret_cast<ncclComm_t>(ctx->comm), st);
+        // exchange the per-shard lists of pods [pr0, pr1) and merge across ranks
+        auto comm = reinterpret_cast<ncclComm_t>(ctx->comm);
+        ncclResult_t r = ncclGroupStart();
+        if (r == ncclSuccess)
+            r = ncclAllGather(ctx->cand_key.as<uint64_t>() + (size_t)pr0 * KC,
+                              ctx->gather.as<uint64_t>(), (size_t)np * KC, ncclUint64, comm, st);
+        if (r == ncclSuccess)
+            r = ncclAllGather(ctx->cand_bound.as<uint64_t>() + pr0, ctx->gbound.as<uint64_t>(),
+                              (size_t)np, ncclUint64, comm, st);
+        ncclResult_t r2 = ncclGroupEnd();
+        if (r == ncclSuccess) r = r2;
         if (r != ncclSuccess)
             return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-        HIPCK(nas::launch_merge(st, ctx->gather.as<uint64_t>(), ctx->world, (int64_t)cnt, pr0,
-                                p_lo, p_hi - p_lo, ctx->cand_key.as<uint64_t>()));
+        HIPCK(nas::launch_merge(st, ctx->gather.as<uint64_t>(), ctx->gbound.as<uint64_t>(),
+                                ctx->world, (int64_t)np * KC, np, pr0, p_lo, p_hi - p_lo,
+                                ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>()));
     }
     hipEvent_t e3 = tm.mark();
     tm.span(T_FIT, e0, e1);
@@ -221,13 +230,16 @@ int alloc_extended(nas_ctx *ctx) {
     const size_t chunks = ctx->Mp / 64;
     OK(nas::ensure(ctx, ctx->mask, chunks * ctx->Pp * 8));
     OK(nas::ensure(ctx, ctx->partial, (size_t)(ctx->Mp / nas::COST_BM) * ctx->Pp * KC * 8));
+    OK(nas::ensure(ctx, ctx->pbound, (size_t)(ctx->Mp / nas::COST_BM) * ctx->Pp * 8));
     OK(nas::ensure(ctx, ctx->cand_key, (size_t)ctx->Pp * KC * 8));
-    OK(nas::ensure(ctx, ctx->cand_node, (size_t)ctx->Pp * KC * 4));
-    OK(nas::ensure(ctx, ctx->cand_cnt, (size_t)ctx->Pp * 4));
+    OK(nas::ensure(ctx, ctx->cand_bound, (size_t)ctx->Pp * 8));
     OK(nas::ensure(ctx, ctx->out_node, (size_t)ctx->Pp * 4));
     OK(nas::ensure(ctx, ctx->out_cost_i, (size_t)ctx->Pp * 4));
     OK(nas::ensure(ctx, ctx->status, 256));
-    if (ctx->world > 1) OK(nas::ensure(ctx, ctx->gather, (size_t)ctx->world * ctx->Pp * KC * 8));
+    if (ctx->world > 1) {
+        OK(nas::ensure(ctx, ctx->gather, (size_t)ctx->world * ctx->Pp * KC * 8));
+        OK(nas::ensure(ctx, ctx->gbound, (size_t)ctx->world * ctx->Pp * 8));
+    }
     if (!ctx->host_status.p) {
         HIPCK(hipHostMalloc(&ctx->host_status.p, 256, hipHostMallocDefault));
         ctx->host_status.bytes = 256;
@@ -277,8 +289,8 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->snap[5], &ctx->order1, &ctx->pos1, &ctx->order2, &ctx->pos2,
                       &ctx->pod_snap, &ctx->best, &ctx->winners, &ctx->snap_best, &ctx->snap_win,
                       &ctx->Lt, &ctx->WA, &ctx->cap0, &ctx->cap, &ctx->req, &ctx->mask,
-                      &ctx->partial, &ctx->cand_key, &ctx->gather, &ctx->cand_node,
-                      &ctx->cand_cnt, &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
+                      &ctx->partial, &ctx->pbound, &ctx->cand_key, &ctx->cand_bound,
+                      &ctx->gather, &ctx->gbound, &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
                       &ctx->status, &ctx->scratch};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
@@ -589,7 +601,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     int p = 0, rounds = 0;
     while (true) {
         hipEvent_t c0 = tm.mark();
-        HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_cnt.as<int32_t>(),
+        HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, p, ctx->P, ctx->cap.as<int32_t>(),
                                  ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
                                  ctx->status.as<int32_t>()));
@@ -638,19 +650,21 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
 }
 
 int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i, float *cand_cost_f,
-                       int32_t *count) {
+                       int32_t *count, int32_t *complete) {
     OK(bind(ctx));
     if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
     const int P = ctx->P;
-    std::vector<uint64_t> keys((size_t)P * KC);
+    std::vector<uint64_t> keys((size_t)P * KC), bounds(P);
     HIPCK(hipMemcpyAsync(keys.data(), ctx->cand_key.p, keys.size() * 8, hipMemcpyDeviceToHost,
+                         ctx->stream));
+    HIPCK(hipMemcpyAsync(bounds.data(), ctx->cand_bound.p, bounds.size() * 8, hipMemcpyDeviceToHost,
                          ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
     for (int p = 0; p < P; ++p) {
         int c = 0;
         for (int j = 0; j < KC; ++j) {
             const uint64_t k = keys[(size_t)p * KC + j];
-            const bool ok = k != nas::KEY_INVALID;
+            const bool ok = k != nas::KEY_INVALID && k <= bounds[p];  // exact prefix only
             c += ok;
             if (cand_node) cand_node[(size_t)p * KC + j] = ok ? (int32_t)(uint32_t)k : -1;
             const uint32_t raw = (uint32_t)(k >> 32);
@@ -660,6 +674,7 @@ int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i, f
             if (cand_cost_f) cand_cost_f[(size_t)p * KC + j] = ok ? decode_cost(raw, ctx->dtype) : 0.f;
         }
         if (count) count[p] = c;
+        if (complete) complete[p] = bounds[p] == nas::KEY_INVALID;
     }
     return NAS_OK;
 }

@@ -70,11 +70,12 @@ struct nas_ctx {
     nas::DevBuf cap0, cap;   // [3][N] int32 (initial, working)
     nas::DevBuf req;         // [3][Pp] int32
     nas::DevBuf mask;        // [ceil(Mp/64)][Pp] uint64, local nodes
-    nas::DevBuf partial;     // [Mp/BM][Pp][KC] uint64 keys
+    nas::DevBuf partial;     // [Mp/BM][Pp][KC] uint64 keys per node tile
+    nas::DevBuf pbound;      // [Mp/BM][Pp] uint64 exactness bound per node tile
     nas::DevBuf cand_key;    // [Pp][KC] uint64 (global node ids), after merge
+    nas::DevBuf cand_bound;  // [Pp] uint64
     nas::DevBuf gather;      // [world][Pp][KC] uint64 (multi-GPU exchange)
-    nas::DevBuf cand_node;   // [Pp][KC] int32
-    nas::DevBuf cand_cnt;    // [Pp] int32
+    nas::DevBuf gbound;      // [world][Pp] uint64
     nas::DevBuf out_node, out_cost_f, out_cost_i;  // [Pp]
     nas::DevBuf status;      // small device scratch for commit control
     nas::DevBuf host_status; // pinned
@@ -105,12 +106,11 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
 
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
-                            uint64_t *partial, int node_base);
-hipError_t launch_merge(hipStream_t st, const uint64_t *partial, int n_lists, int64_t list_stride,
-                        int src_p0, int p0, int np, uint64_t *cand_key);
-hipError_t launch_unpack(hipStream_t st, const uint64_t *cand_key, int p0, int np, int dtype,
-                         int32_t *cand_node, int32_t *cand_cnt);
-hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const int32_t *cand_cnt,
+                            uint64_t *partial, uint64_t *pbound, int node_base);
+hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
+                        int64_t stride, int64_t bstride, int src_p0, int p0, int np,
+                        uint64_t *cand_key, uint64_t *cand_bound);
+hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost_i, int32_t *status);
 

@@ -17,11 +17,12 @@ int main(int argc, char **argv) {
     const int P = argc > 2 ? atoi(argv[2]) : 100000;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
     const int Mp = (int)round_up(N, 256), Kp = (int)round_up(N, 128), Pp = (int)round_up(P, 256);
-    void *Lt, *WA, *mask, *partial;
+    void *Lt, *WA, *mask, *partial, *pbound;
     CK(hipMalloc(&Lt, (size_t)Mp * Kp));
     CK(hipMalloc(&WA, (size_t)Pp * Kp));
     CK(hipMalloc(&mask, (size_t)(Mp / 64) * Pp * 8));
-    CK(hipMalloc(&partial, (size_t)(Mp / 256) * Pp * 32 + (size_t)(Mp / 256) * (Pp / 256) * 512 * 4));
+    CK(hipMalloc(&pbound, (size_t)(Mp / 256) * Pp * 8));
+    CK(hipMalloc(&partial, (size_t)(Mp / 256) * Pp * 64 + (size_t)(Mp / 256) * (Pp / 256) * 512 * 4));
     std::vector<signed char> h((size_t)Pp * Kp);
     for (size_t i = 0; i < h.size(); ++i) h[i] = (signed char)((i * 2654435761u >> 13) % 7 - 3);
     CK(hipMemcpy(WA, h.data(), (size_t)Pp * Kp, hipMemcpyHostToDevice));
@@ -40,7 +41,7 @@ int main(int argc, char **argv) {
             CK(hipEventRecord(a));
 #define L(E) k_cost_topk<NAS_DT_I8, E><<<n_mt * n_nt, THREADS, LDS_BYTES>>>( \
                     (const unsigned char *)Lt, (const unsigned char *)WA, Kp, n_mt, n_nt, 0, Pp, \
-                    (const u64 *)mask, (u64 *)partial, 0)
+                    (const u64 *)mask, (u64 *)partial, (u64 *)pbound, 0)
             if (v == 0) L(0); else if (v == 1) L(1); else L(2);
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));

@@ -178,8 +178,10 @@ class Engine:
         ci = np.empty((P, K), np.int64)
         cf = np.empty((P, K), np.float32)
         cnt = np.empty(P, np.int32)
-        self._ck(self._L.nas_get_candidates(self._h, ptr(node), ptr(ci), ptr(cf), ptr(cnt)))
-        return node, ci, cf, cnt
+        complete = np.empty(P, np.int32)
+        self._ck(self._L.nas_get_candidates(self._h, ptr(node), ptr(ci), ptr(cf), ptr(cnt),
+                                            ptr(complete)))
+        return node, ci, cf, cnt, complete.astype(bool)
 
     def place(self, want_cost=True):
         P = self.n_pods

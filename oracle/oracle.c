@@ -368,22 +368,24 @@ int or_place(int P, int N, int dtype, const void *WA, const void *L, const int32
 
 /*
  * Commit from candidate lists (what the GPU commit kernel does): pods in
- * order take their first candidate that still fits.  A pod whose k
- * candidates all fail while its list was full (count == k) needs a rescore:
- * return its index in *stop (and commit nothing for it); *stop = P when all
- * pods were committed.  A pod with count < k whose candidates all fail is
- * unschedulable (NAS_EMPTY).
+ * order take their first candidate (of the count[p] usable ones) that still
+ * fits.  A pod whose usable candidates all fail while its list is not
+ * complete (complete[p] == 0; NULL means complete iff count < k) needs a
+ * rescore: return its index in *stop (and commit nothing for it); *stop = P
+ * when all pods were committed.  A complete list whose candidates all fail
+ * means the pod is unschedulable (NAS_EMPTY).
  */
-void or_commit(int P, int k, const int32_t *cand_node, const int32_t *count, const int32_t *rc,
-               const int32_t *rm, const int32_t *rp, int32_t *fc, int32_t *fm, int32_t *fp,
-               int32_t *node_out, int32_t *slot_out, int *stop) {
+void or_commit(int P, int k, const int32_t *cand_node, const int32_t *count,
+               const int32_t *complete, const int32_t *rc, const int32_t *rm, const int32_t *rp,
+               int32_t *fc, int32_t *fm, int32_t *fp, int32_t *node_out, int32_t *slot_out,
+               int *stop) {
     for (int p = 0; p < P; ++p) {
         int chosen = -1, slot = -1;
         for (int j = 0; j < count[p]; ++j) {
             int n = cand_node[(size_t)p * k + j];
             if (fits(rc[p], rm[p], rp[p], fc[n], fm[n], fp[n])) { chosen = n; slot = j; break; }
         }
-        if (chosen < 0 && count[p] == k) { *stop = p; return; }
+        if (chosen < 0 && !(complete ? complete[p] : count[p] < k)) { *stop = p; return; }
         node_out[p] = chosen < 0 ? OR_EMPTY : chosen;
         if (slot_out) slot_out[p] = slot;
         if (chosen >= 0) { fc[chosen] -= rc[p]; fm[chosen] -= rm[p]; fp[chosen] -= rp[p]; }

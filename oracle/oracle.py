@@ -157,8 +157,9 @@ def place(WA, L, req, free, dtype):
     return node, (ci if ci is not None else cd), np.stack(fcols, axis=1)
 
 
-def commit(cand_node, count, req, free):
-    """Commit from candidate lists. Returns (node[P], slot[P], free_after, stop)."""
+def commit(cand_node, count, req, free, complete=None):
+    """Commit from candidate lists. Returns (node[P], slot[P], free_after, stop).
+    complete[p]: list holds every fitting node (default: count < k)."""
     cand_node = _c(cand_node, np.int32)
     P, k = cand_node.shape
     req = _c(req, np.int32)
@@ -168,6 +169,8 @@ def commit(cand_node, count, req, free):
     node = np.full(P, -3, np.int32)
     slot = np.full(P, -1, np.int32)
     stop = ctypes.c_int(0)
-    lib().or_commit(P, k, _ptr(cand_node), _ptr(_c(count, np.int32)), *[_ptr(a) for a in rcols],
+    comp = None if complete is None else _c(complete, np.int32)
+    lib().or_commit(P, k, _ptr(cand_node), _ptr(_c(count, np.int32)), _ptr(comp),
+                    *[_ptr(a) for a in rcols],
                     *[_ptr(a) for a in fcols], _ptr(node), _ptr(slot), ctypes.byref(stop))
     return node, slot, np.stack(fcols, axis=1), stop.value

@@ -53,18 +53,25 @@ def test_fit_mask(engine, P, N):
 @pytest.mark.parametrize("P,N,lo,hi", [(256, 256, 0, 20), (300, 70, -20, 20), (1000, 1000, 0, 127),
                                        (700, 1500, -128, 127), (2048, 4096, 0, 8)])
 def test_candidates_i8_exact(engine, P, N, lo, hi):
+    """The usable prefix of each list (count entries) is exactly the oracle's
+    ranking of fitting nodes by (cost, node), with exact integer costs; it
+    holds at least min(4, #fitting) entries; complete lists hold them all."""
     rng = np.random.default_rng(P + N)
     WA, L, free, req = cluster(rng, P, N, lo=lo, hi=hi, cap_scale=0.1)
     upload(engine, WA, L, free, req, "i8")
     engine.score()
-    node, ci, cf, cnt = engine.candidates()
+    node, ci, cf, cnt, complete = engine.candidates()
     cost = oracle.cost(WA, L, "i8")
     mask = oracle.fit_mask(req, free)
-    wn, wc, wcnt = oracle.topk(cost, mask, 4)
-    assert (cnt == wcnt).all()
-    assert (node == wn).all()
-    valid = wn >= 0
-    assert (ci[valid] == wc[valid]).all()
+    wn, wc, wcnt = oracle.topk(cost, mask, 8)
+    assert (cnt >= np.minimum(4, wcnt)).all()
+    for p in range(P):
+        c = cnt[p]
+        assert node[p, :c].tolist() == wn[p, :c].tolist(), p
+        assert ci[p, :c].tolist() == wc[p, :c].tolist(), p
+        assert (node[p, c:] == -1).all()
+        if complete[p]:  # nothing dropped: the list is every fitting node
+            assert c == wcnt[p] < 8
 
 
 @pytest.mark.parametrize("P,N,cap", [(500, 200, 0.3), (1200, 333, 0.05), (3000, 1000, 0.02),
@@ -121,17 +128,18 @@ def test_cost_bf16_random_within_tolerance(engine):
     WA, L, free, req = cluster(rng, P, N, dtype="bf16", int_valued=False, cap_scale=1.0)
     upload(engine, WA, L, free, req, "bf16")
     engine.score()
-    node, _, cf, cnt = engine.candidates()
+    node, _, cf, cnt, _ = engine.candidates()
     cost = oracle.cost(WA, L, "bf16")
     mask = oracle.fit_mask(req, free)
-    wn, wc, wcnt = oracle.topk(cost, mask, 4)
-    assert (cnt == wcnt).all()
+    wn, wc, wcnt = oracle.topk(cost, mask, 8)
+    assert (cnt >= np.minimum(4, wcnt)).all()
     rows = np.arange(P)[:, None]
+    usable = node >= 0
     exact = cost[rows, np.maximum(node, 0)]
     rel = np.abs(cf.astype(np.float64) - exact) / np.abs(exact)
-    assert rel[node >= 0].max() <= REL_TOL
+    assert rel[usable].max() <= REL_TOL
     # the GPU's j-th candidate is a true j-th best up to the tolerance
-    assert (np.abs(exact - wc) <= REL_TOL * np.abs(wc))[node >= 0].all()
+    assert (np.abs(exact - wc) <= REL_TOL * np.abs(wc))[usable].all()
 
 
 def test_csr_traffic_matches_dense(engine):
@@ -175,7 +183,7 @@ def test_synthetic_cluster_sampled(engine):
     N, P = 2048, 8192
     engine.synth_cluster(0x4E4153, N, P, "i8", peers=8)
     engine.score()
-    node, ci, _, cnt = engine.candidates()
+    node, ci, _, cnt, complete = engine.candidates()
     rng = np.random.default_rng(0)
     pods = np.sort(rng.choice(P, 64, replace=False))
     _, L, cap, req = engine.read_inputs(0, 0, want_L=True)
@@ -183,11 +191,18 @@ def test_synthetic_cluster_sampled(engine):
         WA, _, _, _ = engine.read_inputs(int(p), 1, want_L=False)
         cost = oracle.cost(WA, L, "i8")
         mask = oracle.fit_mask(req[p:p + 1], cap)
-        wn, wc, wcnt = oracle.topk(cost, mask, 4)
-        assert cnt[p] == wcnt[0] and (node[p] == wn[0]).all() and (ci[p][: cnt[p]] == wc[0][: cnt[p]]).all()
+        wn, wc, wcnt = oracle.topk(cost, mask, 8)
+        c = cnt[p]
+        assert c >= min(4, wcnt[0])
+        assert node[p, :c].tolist() == wn[0, :c].tolist()
+        assert ci[p, :c].tolist() == wc[0, :c].tolist()
     engine.reset_capacity()
     placed, _, _ = engine.place()
-    want, _, wfree, stop = oracle.commit(node, cnt, req, cap)
-    assert stop == P  # no rescore needed on this workload
-    assert placed.tolist() == want.tolist()
-    assert (engine.get_capacity() == wfree).all()
+    rounds = engine.timings()["rescore_rounds"]
+    want, _, wfree, stop = oracle.commit(node, cnt, req, cap, complete)
+    if rounds == 0:
+        assert stop == P
+        assert placed.tolist() == want.tolist()
+        assert (engine.get_capacity() == wfree).all()
+    else:  # the GPU rescored from `stop` on: the prefix before it must agree
+        assert placed[:stop].tolist() == want[:stop].tolist()
