@@ -31,6 +31,9 @@ PEAK_I8_TOPS = 5033.2     # dense int8 MFMA, 256 CU x 4 SIMD x 2048 op/clk x 2.4
 PEAK_BF16_TFLOPS = 2516.6  # dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # HBM3E spec (MI355X_MICROARCH.md)
 SEED = 0x4E4153
+# HBM bytes per k_cost_topk launch from rocprofv3 PMC passes (profiles/, see
+# DESIGN.md): (FETCH_SIZE x 2 gfx950 correction + WRITE_SIZE) in bytes, or None
+PMC_TRAFFIC = {}
 
 
 def parse():
@@ -45,7 +48,7 @@ def parse():
     ap.add_argument("--no-reference-mode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=12.0)
-    ap.add_argument("--only", choices=["place", "vote"], default=None,
+    ap.add_argument("--only", choices=["place", "vote", "score"], default=None,
                     help="profile helper: run only one path")
     return ap.parse_args()
 
@@ -105,29 +108,41 @@ def bench_place(args, d, eng):
         uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
         eng.comm_init(uid, d.rank, d.world)
     eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
-    acc = {"cost_ms": 0.0, "fit_ms": 0.0, "merge_ms": 0.0, "commit_ms": 0.0, "total_ms": 0.0,
-           "cost_launches": 0, "rescore_rounds": 0, "unschedulable": 0}
-    state = {"n": 0, "node": None}
+    keys = ("cost_ms", "fit_ms", "merge_ms", "commit_ms", "total_ms", "cost_launches",
+            "rescore_rounds", "unschedulable")
+    acc = dict.fromkeys(keys, 0.0)
+    state = {"node": None}
 
     def step():
         eng.reset_capacity()
         node, _, score = eng.place(want_cost=True)
         t = eng.timings()
-        if state["n"] >= 0:
-            for k in acc:
-                acc[k] += t[k]
-            state["n"] += 1
+        for k in keys:
+            acc[k] += t[k]
         state["node"] = node
 
     for _ in range(args.warmup):
         step()
-    for k in acc:
-        acc[k] = 0
-    state["n"] = 0
+    for k in keys:
+        acc[k] = 0.0
     elapsed = time_steps(d, step, args.steps, 0)
-    n = max(1, state["n"])
-    per = {k: v / n for k, v in acc.items()}
+    per = {k: v / args.steps for k, v in acc.items()}
     return elapsed, per, state["node"]
+
+
+def bench_cost_kernel(args, d, eng):
+    """Roofline of the dominant kernel: one full-size scoring pass (fit + one
+    k_cost_topk launch over all pods + merge) on one stream, HIP events
+    around the k_cost_topk launch."""
+    eng.reset_capacity()
+    eng.score()
+    ms = []
+    for _ in range(max(3, args.steps)):
+        eng.score()
+        t = eng.timings()
+        assert t["cost_launches"] == 1
+        ms.append(t["cost_ms"])
+    return float(np.median(ms)), ms
 
 
 def bench_vote(args, d, eng):
@@ -221,27 +236,33 @@ def main():
                                   f"traffic, racks of 32 / zones of 16 racks, {args.peers} "
                                   f"peers per pod, clusterloader2-shaped requests",
                       "nodes": N, "pods": P, "parallelism": f"node-sharded x{d.world}",
-                      "candidates_per_pod": 4}}
+                      "candidates_per_pod": 8}}
     gpu_nodes = None
-    if args.only != "vote":
+    if args.only not in ("vote", "score"):
         elapsed, per, gpu_nodes = bench_place(args, d, eng)
-        ms = elapsed * 1e3 / args.steps
         out["value"] = P * N / (elapsed / args.steps)
-        out["ms_per_step"] = ms
+        out["ms_per_step"] = elapsed * 1e3 / args.steps
         out["placements_per_s"] = P / (elapsed / args.steps)
+        out["stages_ms"] = {k: per[k] for k in ("fit_ms", "cost_ms", "merge_ms", "commit_ms",
+                                                "total_ms")}
+        out["stages_note"] = ("device-side sums per step; scoring runs in 8192-pod chunks on two "
+                              "streams with the commit pipelined on a third, so stages overlap")
+        out["rescore_rounds"] = per["rescore_rounds"]
+        out["unschedulable"] = per["unschedulable"]
+    if args.only != "vote":
+        if gpu_nodes is None:
+            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+        cost_ms, samples = bench_cost_kernel(args, d, eng)
         nloc = N // d.world
-        ops = 2.0 * P * N * nloc * max(1, per["cost_launches"]) / max(1, per["cost_launches"])
-        cost_ms = per["cost_ms"] / max(1, per["cost_launches"])
+        ops = 2.0 * P * N * nloc
         achieved = ops / (cost_ms * 1e-3) / 1e12
         peak = PEAK_I8_TOPS if args.dtype == "i8" else PEAK_BF16_TFLOPS
         out["roofline"] = {"kernel": "k_cost_topk", "bound": "mfma", "achieved": achieved,
                            "peak": peak, "unit": "TOPS" if args.dtype == "i8" else "TFLOP/s",
-                           "frac": achieved / peak, "traffic": None,
-                           "launch_ms": cost_ms, "ops_per_launch": ops}
-        out["stages_ms"] = {k: per[k] for k in ("fit_ms", "cost_ms", "merge_ms", "commit_ms",
-                                                "total_ms")}
-        out["rescore_rounds"] = per["rescore_rounds"]
-        out["unschedulable"] = per["unschedulable"]
+                           "frac": achieved / peak, "traffic": PMC_TRAFFIC.get(args.dtype),
+                           "launch_ms": cost_ms, "ops_per_launch": ops,
+                           "note": "one launch over all pods x this rank's node columns "
+                                   "(nas_score), HIP events on its stream; 2*P*N*N_local ops"}
     if not args.no_reference_mode and args.only != "place":
         elapsed, vote_ms, S, ref = bench_vote(args, d, eng)
         bytes_launch = 48.0 * N * S

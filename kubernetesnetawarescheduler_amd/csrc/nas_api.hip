@@ -61,6 +61,7 @@ int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes) {
 namespace {
 
 constexpr int RESCORE_PODS = 1024;  // pods rescored per commit stop (multiple of COST_BN)
+constexpr int CHUNK_PODS = 32 * nas::COST_BN;  // pods per pipelined scoring chunk
 
 int bind(nas_ctx *ctx) {
     if (!ctx) return NAS_ERR_ARG;
@@ -77,11 +78,6 @@ int64_t kpad(int n, int dtype) { return nas::round_up(n, dtype == NAS_DT_I8 ? 12
 struct Timer {
     nas_ctx *ctx;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> spans;
-    static std::vector<hipEvent_t> &pool(nas_ctx *) {
-        static thread_local std::vector<hipEvent_t> p;
-        return p;
-    }
-    size_t used = 0;
     std::vector<hipEvent_t> evs;
     explicit Timer(nas_ctx *c) : ctx(c) {}
     ~Timer() {
@@ -93,9 +89,9 @@ struct Timer {
         evs.push_back(e);
         return e;
     }
-    hipEvent_t mark() {
+    hipEvent_t mark(hipStream_t st = nullptr) {
         hipEvent_t e = ev();
-        if (e) (void)hipEventRecord(e, ctx->stream);
+        if (e) (void)hipEventRecord(e, st ? st : ctx->stream);
         return e;
     }
     void span(int which, hipEvent_t a, hipEvent_t b) { spans.push_back({which, {a, b}}); }
@@ -181,21 +177,24 @@ int check_extended(nas_ctx *ctx) {
     return NAS_OK;
 }
 
-// scoring for pods [p_lo, p_hi): fit -> cost/top-k -> merge (-> exchange)
-int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi) {
-    hipStream_t st = ctx->stream;
+// scoring for pods [p_lo, p_hi) on stream st against capacity `cap`:
+// fit -> cost/top-k -> merge (-> exchange)
+int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nullptr,
+                const int32_t *cap = nullptr) {
+    if (!st) st = ctx->stream;
+    if (!cap) cap = ctx->cap.as<int32_t>();
     const int pr0 = p_lo / nas::COST_BN * nas::COST_BN;
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
     const int np = pr1 - pr0;
     auto *mask = ctx->mask.as<uint64_t>();
-    hipEvent_t e0 = tm.mark();
-    HIPCK(nas::launch_fit(st, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
+    hipEvent_t e0 = tm.mark(st);
+    HIPCK(nas::launch_fit(st, cap, ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
                           ctx->req.as<int32_t>(), ctx->P, ctx->Pp, p_lo, p_hi - p_lo, mask));
-    hipEvent_t e1 = tm.mark();
+    hipEvent_t e1 = tm.mark(st);
     HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, ctx->Pp,
                                 pr0, np, mask, ctx->partial.as<uint64_t>(),
                                 ctx->pbound.as<uint64_t>(), ctx->Nloc0));
-    hipEvent_t e2 = tm.mark();
+    hipEvent_t e2 = tm.mark(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
                             (int64_t)ctx->Pp * KC, ctx->Pp, 0, p_lo, p_hi - p_lo,
@@ -218,7 +217,7 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi) {
                                 ctx->world, (int64_t)np * KC, np, pr0, p_lo, p_hi - p_lo,
                                 ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>()));
     }
-    hipEvent_t e3 = tm.mark();
+    hipEvent_t e3 = tm.mark(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
     tm.span(T_MERGE, e2, e3);
@@ -236,6 +235,7 @@ int alloc_extended(nas_ctx *ctx) {
     OK(nas::ensure(ctx, ctx->out_node, (size_t)ctx->Pp * 4));
     OK(nas::ensure(ctx, ctx->out_cost_i, (size_t)ctx->Pp * 4));
     OK(nas::ensure(ctx, ctx->status, 256));
+    OK(nas::ensure(ctx, ctx->cap_snap, (size_t)3 * ctx->N * 4));
     if (ctx->world > 1) {
         OK(nas::ensure(ctx, ctx->gather, (size_t)ctx->world * ctx->Pp * KC * 8));
         OK(nas::ensure(ctx, ctx->gbound, (size_t)ctx->world * ctx->Pp * 8));
@@ -273,7 +273,9 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
     if (!ctx) return NAS_ERR_NOMEM;
     ctx->device = dev;
     if (hipSetDevice(dev) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream_commit, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return NAS_ERR_HIP;
     }
@@ -288,7 +290,7 @@ void nas_destroy(nas_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->snap[0], &ctx->snap[1], &ctx->snap[2], &ctx->snap[3], &ctx->snap[4],
                       &ctx->snap[5], &ctx->order1, &ctx->pos1, &ctx->order2, &ctx->pos2,
                       &ctx->pod_snap, &ctx->best, &ctx->winners, &ctx->snap_best, &ctx->snap_win,
-                      &ctx->Lt, &ctx->WA, &ctx->cap0, &ctx->cap, &ctx->req, &ctx->mask,
+                      &ctx->Lt, &ctx->WA, &ctx->cap0, &ctx->cap, &ctx->cap_snap, &ctx->req, &ctx->mask,
                       &ctx->partial, &ctx->pbound, &ctx->cand_key, &ctx->cand_bound,
                       &ctx->gather, &ctx->gbound, &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
                       &ctx->status, &ctx->scratch};
@@ -297,6 +299,8 @@ void nas_destroy(nas_ctx *ctx) {
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
     if (ctx->comm) (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(ctx->comm));
     (void)hipStreamDestroy(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream2);
+    (void)hipStreamDestroy(ctx->stream_commit);
     delete ctx;
 }
 
@@ -594,32 +598,53 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     OK(alloc_extended(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
-    hipStream_t st = ctx->stream;
-    hipEvent_t t0 = tm.mark();
-    OK(score_range(ctx, tm, 0, ctx->P));
-    int32_t *hs = ctx->host_status.as<int32_t>();
-    int p = 0, rounds = 0;
-    while (true) {
-        hipEvent_t c0 = tm.mark();
-        HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
-                                 ctx->req.as<int32_t>(), ctx->Pp, p, ctx->P, ctx->cap.as<int32_t>(),
-                                 ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
-                                 ctx->status.as<int32_t>()));
-        hipEvent_t c1 = tm.mark();
-        tm.span(T_COMMIT, c0, c1);
-        HIPCK(hipMemcpyAsync(hs, ctx->status.p, 4, hipMemcpyDeviceToHost, st));
-        HIPCK(hipStreamSynchronize(st));
-        const int stop = hs[0];
-        if (stop < p || stop > ctx->P) return nas::fail(ctx, NAS_ERR_HIP, "commit status corrupt");
-        if (stop >= ctx->P) break;
-        // pod `stop` exhausted its candidates: rescore a window against the
-        // current capacity (lists computed now stay valid for later pods)
-        ++rounds;
-        if (rounds > ctx->P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
-        OK(score_range(ctx, tm, stop, std::min(ctx->P, stop + RESCORE_PODS)));
-        p = stop;
+    hipStream_t st = ctx->stream, sc = ctx->stream_commit;
+    const int P = ctx->P, N = ctx->N;
+    int32_t *halt = ctx->status.as<int32_t>();
+    hipEvent_t t0 = tm.mark(st);
+    // the scoring pass filters against the capacity at entry, while the
+    // commit walks (stream_commit) consume the working capacity behind it
+    HIPCK(hipMemcpyAsync(ctx->cap_snap.p, ctx->cap.p, (size_t)3 * N * 4, hipMemcpyDeviceToDevice, st));
+    HIPCK(hipMemsetAsync(halt, 0xff, 16, st));  // halt = -1
+    hipEvent_t ready = tm.mark(st);
+    HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
+    HIPCK(hipStreamWaitEvent(sc, ready, 0));
+    for (int c = 0, lo = 0; lo < P; ++c, lo += CHUNK_PODS) {
+        const int hi = std::min(P, lo + CHUNK_PODS);
+        // two scoring streams: a chunk's tail blocks overlap the next chunk
+        // (multi-GPU keeps one stream so every rank issues its collectives in order)
+        hipStream_t ss = (ctx->world == 1 && (c & 1)) ? ctx->stream2 : st;
+        OK(score_range(ctx, tm, lo, hi, ss, ctx->cap_snap.as<int32_t>()));
+        HIPCK(hipStreamWaitEvent(sc, tm.mark(ss), 0));
+        hipEvent_t c0 = tm.mark(sc);
+        HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                                 ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
+                                 ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt));
+        tm.span(T_COMMIT, c0, tm.mark(sc));
     }
-    const int P = ctx->P;
+    HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
+    HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
+    int32_t *hs = ctx->host_status.as<int32_t>();
+    HIPCK(hipMemcpyAsync(hs, halt, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    int rounds = 0;
+    while (hs[0] >= 0) {
+        // pod `stop` exhausted its candidates: rescore a window against the
+        // current capacity (lists computed now stay valid for later pods),
+        // then walk on from it
+        const int stop = hs[0];
+        if (stop >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
+        if (++rounds > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
+        OK(score_range(ctx, tm, stop, std::min(P, stop + RESCORE_PODS)));
+        HIPCK(hipMemsetAsync(halt, 0xff, 16, st));
+        hipEvent_t c0 = tm.mark(st);
+        HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                                 ctx->req.as<int32_t>(), ctx->Pp, stop, P, ctx->cap.as<int32_t>(), N,
+                                 ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt));
+        tm.span(T_COMMIT, c0, tm.mark(st));
+        HIPCK(hipMemcpyAsync(hs, halt, 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+    }
     std::vector<uint32_t> raw;
     HIPCK(hipMemcpyAsync(node_out, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
     if (cost_out || int_score_out) {

@@ -39,7 +39,9 @@ constexpr uint64_t KEY_INVALID = ~0ull;
 
 struct nas_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // main stream (uploads, scoring, results)
+    hipStream_t stream2 = nullptr;     // second scoring stream (chunk tails overlap)
+    hipStream_t stream_commit = nullptr;  // commit walks, pipelined behind scoring
     std::string err;
     hipEvent_t ev[12] = {};
     nas_timings timings = {};
@@ -68,6 +70,7 @@ struct nas_ctx {
     nas::DevBuf Lt;          // [Mp][Kp] elements: Lt[i][m] = L[m][Nloc0 + i]
     nas::DevBuf WA;          // [Pp][Kp] elements
     nas::DevBuf cap0, cap;   // [3][N] int32 (initial, working)
+    nas::DevBuf cap_snap;    // [3][N] working capacity at the start of nas_place
     nas::DevBuf req;         // [3][Pp] int32
     nas::DevBuf mask;        // [ceil(Mp/64)][Pp] uint64, local nodes
     nas::DevBuf partial;     // [Mp/BM][Pp][KC] uint64 keys per node tile
@@ -112,7 +115,7 @@ hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bo
                         uint64_t *cand_key, uint64_t *cand_bound);
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
-                         int32_t *out_node, int32_t *out_cost_i, int32_t *status);
+                         int32_t *out_node, int32_t *out_cost_i, int32_t *halt);
 
 hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
                               int nloc, int Mp, int Kp, void *Lt);
