@@ -42,8 +42,21 @@ constexpr int BM = COST_BM;   // nodes per tile
 constexpr int BN = COST_BN;   // pods per tile
 constexpr int BKB = COST_BKB; // bytes of K per LDS stage (full 128-byte lines)
 constexpr int STAGE_BYTES = (BM + BN) * BKB;  // 64 KiB
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;    // 128 KiB, double-buffered
-constexpr int GM = 4;  // node tiles per L2 group
+constexpr int TILE_BYTES = BM * BKB;          // 32 KiB: one operand, one stage
+#ifndef COST_PIPE
+#define COST_PIPE 0
+#endif
+#ifndef COST_GM
+#define COST_GM 4
+#endif
+// PIPE 0: A and B double-buffered (128 KiB).  PIPE 1: A (latency rows, mostly
+// L2/MALL-resident) double-buffered, B (the 1 GB traffic stream, mostly HBM)
+// triple-buffered so its loads get two K-steps of cover (160 KiB, all of LDS).
+template <int PIPE>
+constexpr int lds_bytes() { return PIPE == 0 ? 2 * STAGE_BYTES : 5 * TILE_BYTES; }
+#ifndef COST_SCHED
+#define COST_SCHED 1
+#endif
 
 template <int DT>
 struct Mma;
@@ -100,8 +113,11 @@ struct Top4 {
 
 // EPI != 0 are diagnostic variants for tools/mb_cost.hip: 1 = accumulators
 // kept alive with an empty asm and no epilogue (times the main loop alone),
-// 2 = per-lane top-1 instead of top-4.
-template <int DT, int EPI = 0>
+// 2 = per-lane top-1 instead of top-4.  SCHED selects the k-substep schedule
+// (A/B'd in tools/mb_cost.hip): 0 hipcc's own, 1 pinned MFMA/ds_read
+// interleave, 2 s_setprio(1) around each MFMA cluster, 3 iglp_opt(0),
+// 4 iglp_opt(1).
+template <int DT, int EPI = 0, int SCHED = COST_SCHED, int PIPE = COST_PIPE, int GM = COST_GM>
 __global__ void __launch_bounds__(THREADS, 1)
 k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
@@ -127,6 +143,10 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 
     const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
     const unsigned char *Bg = WA + (size_t)(p0 + nt * BN) * Kb;
+    if constexpr (EPI == 3) {  // diagnostic: every block streams tile (0, 0): all L2 hits
+        Ag = Lt;
+        Bg = WA;
+    }
 
     // LDS-DMA staging: piece j of wave w fills rows (8j + w)*8 .. +8 of A
     // and of B (1 KiB each, lane-linear: lane l -> row + l/8, 16-byte chunk
@@ -135,17 +155,35 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // SOURCE address so fragment reads are bank-conflict free.
     const int srow_in = lane >> 3;
     const int sq = lane & 7;
-    auto stage = [&](int buf, int k0) {
-        unsigned char *As = lds + buf * STAGE_BYTES;
-        unsigned char *Bs = As + BM * BKB;
+    // buffer b of operand A / B (PIPE 0: A|B interleaved per stage; PIPE 1:
+    // A0 A1 B0 B1 B2)
+    auto abuf = [&](int b) -> unsigned char * {
+        return PIPE == 0 ? lds + b * STAGE_BYTES : lds + b * TILE_BYTES;
+    };
+    auto bbuf = [&](int b) -> unsigned char * {
+        return PIPE == 0 ? lds + b * STAGE_BYTES + TILE_BYTES : lds + (2 + b) * TILE_BYTES;
+    };
+    // one 1 KiB LDS-DMA piece (8 rows x 128 B) of operand A / B: piece j of
+    // wave w fills rows (8j + w)*8 .. +8
+    auto pieceA = [&](int buf, int k0, int j) {
+        const int r0 = (j * 8 + w) * 8;
+        const int row = r0 + srow_in;
+        const int c = sq ^ ((row >> 1) & 7);
+        glds16(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
+    };
+    auto pieceB = [&](int buf, int k0, int j) {
+        const int r0 = (j * 8 + w) * 8;
+        const int row = r0 + srow_in;
+        const int c = sq ^ ((row >> 1) & 7);
+        glds16(Bg + (size_t)row * Kb + k0 + c * 16, bbuf(buf) + r0 * BKB);
+    };
+    auto stageA = [&](int buf, int k0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int r0 = (j * 8 + w) * 8;
-            const int row = r0 + srow_in;
-            const int c = sq ^ ((row >> 1) & 7);
-            glds16(Ag + (size_t)row * Kb + k0 + c * 16, As + r0 * BKB);
-            glds16(Bg + (size_t)row * Kb + k0 + c * 16, Bs + r0 * BKB);
-        }
+        for (int j = 0; j < 4; ++j) pieceA(buf, k0, j);
+    };
+    auto stageB = [&](int buf, int k0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pieceB(buf, k0, j);
     };
 
     acc_t acc[4][2];
@@ -155,44 +193,146 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         for (int j = 0; j < 2; ++j) acc[i][j] = acc_t{};
 
     const int fr = lane & 31, fh = lane >> 5;
-    auto compute = [&](int buf) {
-        const unsigned char *As = lds + buf * STAGE_BYTES;
-        const unsigned char *Bs = As + BM * BKB;
-#pragma unroll
-        for (int kk = 0; kk < BKB / 32; ++kk) {
+    // fragments of k-substep kk+1 are read from LDS while the 8 MFMAs of kk
+    // run (register double buffer; the just-in-time schedule hipcc picks on
+    // its own exposes the LDS latency every 4 MFMAs)
+    // compute one K-step from LDS; `piece(kk)` issues the next stage's LDS-DMA
+    // pieces that SCHED 5 spreads across the MFMA stream (their issue cost,
+    // 60-185 cycles each, otherwise stalls the wave at the top of the step)
+    auto compute = [&](int ab, int bbi, auto &&piece) {
+        const unsigned char *As = abuf(ab);
+        const unsigned char *Bs = bbuf(bbi);
+        v4i a[2][4], bb[2][2];
+        auto read = [&](int kk, v4i (&ra)[4], v4i (&rb)[2]) {
             const int c = kk * 2 + fh;
-            v4i a[4], bb[2];
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
                 const int r = wm * 128 + mi * 32 + fr;
-                a[mi] = *reinterpret_cast<const v4i *>(As + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
+                ra[mi] = *reinterpret_cast<const v4i *>(As + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
             }
 #pragma unroll
             for (int ni = 0; ni < 2; ++ni) {
                 const int r = wn * 64 + ni * 32 + fr;
-                bb[ni] = *reinterpret_cast<const v4i *>(Bs + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
+                rb[ni] = *reinterpret_cast<const v4i *>(Bs + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
             }
+        };
+        read(0, a[0], bb[0]);
+#pragma unroll
+        for (int kk = 0; kk < BKB / 32; ++kk) {
+            if constexpr (SCHED == 5) piece(kk);
+            if (kk + 1 < BKB / 32) read(kk + 1, a[(kk + 1) & 1], bb[(kk + 1) & 1]);
+            if constexpr (SCHED == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = M::mma(a[mi], bb[ni], acc[mi][ni]);
+                for (int ni = 0; ni < 2; ++ni)
+                    acc[mi][ni] = M::mma(a[kk & 1][mi], bb[kk & 1][ni], acc[mi][ni]);
+            if constexpr (SCHED == 2) __builtin_amdgcn_s_setprio(0);
+            if constexpr (SCHED == 1) {
+                // pin the interleave: MFMA, LDS read, MFMA, ... (6 reads of
+                // the next k-substep hidden under the 8 MFMAs of this one)
+                if (kk + 1 < BKB / 32) {
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                }
+            }
+            if constexpr (SCHED == 5) {
+                // MFMA, DMA piece, MFMA, LDS read, ... : 2 pieces + 6 reads in 8 MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (kk + 1 < BKB / 32) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (kk + 1 < BKB / 32) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    }
+                } else {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                }
+            }
+            if constexpr (SCHED == 3) __builtin_amdgcn_iglp_opt(0);
+            if constexpr (SCHED == 4) __builtin_amdgcn_iglp_opt(1);
         }
     };
+    auto nopiece = [](int) {};
 
-    // two-stage pipeline: stage t+1 streams in (LDS-DMA) while stage t is read
     const int nk = Kb / BKB;
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-        const int cur = t & 1;
-        if (t + 1 < nk) stage(cur ^ 1, (t + 1) * BKB);
-        compute(cur);
+    if constexpr (EPI == 4 || EPI == 5) {
+        // diagnostic: stage once, then run the K loop on LDS only (4: with
+        // the per-step barrier, 5: without) -- the in-core ceiling
+        stageA(0, 0);
+        stageB(0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int t = 0; t < nk; ++t) {
+            compute(0, 0, nopiece);
+            if constexpr (EPI == 4) {
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+            }
+        }
+    } else if constexpr (PIPE == 0) {
+        // two-stage pipeline: stage t+1 streams in (LDS-DMA) while t is read
+        stageA(0, 0);
+        stageB(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int t = 0; t < nk; ++t) {
+            const int cur = t & 1;
+            const bool more = t + 1 < nk;
+            if constexpr (SCHED == 5) {
+                compute(cur, cur, [&](int kk) {
+                    if (more) {
+                        pieceA(cur ^ 1, (t + 1) * BKB, kk);
+                        pieceB(cur ^ 1, (t + 1) * BKB, kk);
+                    }
+                });
+            } else {
+                if (more) {
+                    stageA(cur ^ 1, (t + 1) * BKB);
+                    stageB(cur ^ 1, (t + 1) * BKB);
+                }
+                compute(cur, cur, nopiece);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    } else {
+        // A one stage ahead, B two stages ahead.  Issue order per step is
+        // A(t+1) then B(t+2), so vmcnt(4) (= B's 4 pieces per wave) leaves
+        // exactly B(t+2) in flight across the barrier; a raw s_barrier (no
+        // __syncthreads, whose fence would drain it) ends the step.
+        stageA(0, 0);
+        stageB(0, 0);
+        if (nk > 1) stageB(1, BKB);
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        int b3 = 0;  // t % 3
+        for (int t = 0; t < nk; ++t) {
+            if (t + 1 < nk) stageA((t + 1) & 1, (t + 1) * BKB);
+            if (t + 2 < nk) stageB(b3 == 0 ? 2 : b3 - 1, (t + 2) * BKB);  // (t+2) % 3
+            compute(t & 1, b3, nopiece);
+            if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            b3 = b3 == 2 ? 0 : b3 + 1;
+        }
         __syncthreads();
     }
 
-    if constexpr (EPI == 1) {
+    if constexpr (EPI == 1 || EPI >= 3) {
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -302,12 +442,13 @@ __global__ void k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bo
 }
 
 #ifdef NAS_DIAG_VARIANTS
-template __global__ void k_cost_topk<NAS_DT_I8, 1>(const unsigned char *, const unsigned char *, int,
-                                                   int, int, int, int, const u64 *, u64 *, u64 *,
-                                                   int);
-template __global__ void k_cost_topk<NAS_DT_I8, 2>(const unsigned char *, const unsigned char *, int,
-                                                   int, int, int, int, const u64 *, u64 *, u64 *,
-                                                   int);
+#define NAS_INST(E, S, PP, G)                                                                      \
+    template __global__ void k_cost_topk<NAS_DT_I8, E, S, PP, G>(                                  \
+        const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
+        u64 *, int);
+NAS_INST(0, 0, 0, 4) NAS_INST(1, 0, 0, 4) NAS_INST(0, 5, 0, 4) NAS_INST(1, 5, 0, 4)
+NAS_INST(3, 5, 0, 4) NAS_INST(0, 1, 0, 4) NAS_INST(0, 5, 0, 8) NAS_INST(4, 0, 0, 4)
+#undef NAS_INST
 #endif
 
 template <int DT>
@@ -317,12 +458,13 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_cost_topk<DT>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           lds_bytes<COST_PIPE>());
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int n_mt = Mp / BM, n_nt = np / BN;
-    k_cost_topk<DT><<<n_mt * n_nt, THREADS, LDS_BYTES, st>>>(
+    k_cost_topk<DT><<<n_mt * n_nt, THREADS, lds_bytes<COST_PIPE>(), st>>>(
         static_cast<const unsigned char *>(Lt), static_cast<const unsigned char *>(WA), Kb, n_mt,
         n_nt, p0, Pp, reinterpret_cast<const u64 *>(mask), reinterpret_cast<u64 *>(partial),
         reinterpret_cast<u64 *>(pbound), node_base);

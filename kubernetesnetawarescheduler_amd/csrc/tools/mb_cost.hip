@@ -6,6 +6,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 using namespace nas;
@@ -16,6 +17,7 @@ int main(int argc, char **argv) {
     const int N = argc > 1 ? atoi(argv[1]) : 10000;
     const int P = argc > 2 ? atoi(argv[2]) : 100000;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const char *vsel = argc > 4 ? argv[4] : "abcdefgh";  // variants to run (a..)
     const int Mp = (int)round_up(N, 256), Kp = (int)round_up(N, 128), Pp = (int)round_up(P, 256);
     void *Lt, *WA, *mask, *partial, *pbound;
     CK(hipMalloc(&Lt, (size_t)Mp * Kp));
@@ -28,26 +30,37 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(WA, h.data(), (size_t)Pp * Kp, hipMemcpyHostToDevice));
     CK(hipMemcpy(Lt, h.data(), (size_t)Mp * Kp, hipMemcpyHostToDevice));
     CK(hipMemset(mask, 0xff, (size_t)(Mp / 64) * Pp * 8));
-    CK(hipFuncSetAttribute((const void *)&k_cost_topk<NAS_DT_I8, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    CK(hipFuncSetAttribute((const void *)&k_cost_topk<NAS_DT_I8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
-    CK(hipFuncSetAttribute((const void *)&k_cost_topk<NAS_DT_I8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    // variants: name, kernel
+    struct V { const char *name; const void *fn; int lds; };
+#define KV(E, S, PP, G) (const void *)&k_cost_topk<NAS_DT_I8, E, S, PP, G>, lds_bytes<PP>()
+    const V vars[] = {{"top4/jit", KV(0, 0, 0, 4)},   {"noepi/jit", KV(1, 0, 0, 4)},
+                      {"top4/spread", KV(0, 5, 0, 4)}, {"noepi/spread", KV(1, 5, 0, 4)},
+                      {"l2hot/spread", KV(3, 5, 0, 4)}, {"top4/pin", KV(0, 1, 0, 4)},
+                      {"top4/spr/g8", KV(0, 5, 0, 8)}, {"ldsonly+bar", KV(4, 0, 0, 4)}};
+    const int nv = sizeof(vars) / sizeof(vars[0]);
+    for (int v = 0; v < nv; ++v)
+        CK(hipFuncSetAttribute(vars[v].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[v].lds));
     const int n_mt = Mp / BM, n_nt = Pp / BN;
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const double ops = 2.0 * N * (double)N * P;
+    const unsigned char *lt = (const unsigned char *)Lt, *wa = (const unsigned char *)WA;
+    const u64 *mk = (const u64 *)mask;
+    u64 *pa = (u64 *)partial, *pb = (u64 *)pbound;
+    int zero = 0;
     for (int r = 0; r < reps; ++r) {
-        for (int v = 0; v < 3; ++v) {
+        for (int v = 0; v < nv; ++v) {
+            if (!strchr(vsel, 'a' + v)) continue;
+            void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero,
+                            (void *)&Pp, &mk, &pa, &pb, &zero};
             CK(hipEventRecord(a));
-#define L(E) k_cost_topk<NAS_DT_I8, E><<<n_mt * n_nt, THREADS, LDS_BYTES>>>( \
-                    (const unsigned char *)Lt, (const unsigned char *)WA, Kp, n_mt, n_nt, 0, Pp, \
-                    (const u64 *)mask, (u64 *)partial, (u64 *)pbound, 0)
-            if (v == 0) L(0); else if (v == 1) L(1); else L(2);
+            CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(THREADS), args, vars[v].lds, 0));
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms;
             CK(hipEventElapsedTime(&ms, a, b));
-            printf("rep %d %-10s %8.3f ms %8.1f TOPS\n", r, v == 0 ? "top4" : v == 1 ? "no-epi" : "top1", ms, ops / ms / 1e9);
+            printf("rep %d %-12s %8.3f ms %8.1f TOPS\n", r, vars[v].name, ms, ops / ms / 1e9);
         }
     }
     return 0;
