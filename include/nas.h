@@ -197,6 +197,18 @@ int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i,
 int nas_comm_unique_id(uint8_t id_out[128]);
 int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world);
 
+/* Node shard without a communicator: this context keeps and scores only node
+ * columns [rank*n/world, (rank+1)*n/world) (call before the extended
+ * uploads).  For hosts that exchange candidate lists themselves (nas_score +
+ * nas_get_candidate_keys, then merge: keep the 8 smallest keys, bound =
+ * min(bounds, kept[7])); nas_place needs nas_comm_init instead. */
+int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world);
+
+/* Raw candidate lists of the last scoring pass: keys[P*8] (orderable cost
+ * << 32 | global node index, ascending; ~0 = empty) and bounds[P] (every
+ * fitting key <= bound is in the list; ~0 = nothing was dropped). */
+int nas_get_candidate_keys(nas_ctx *ctx, uint64_t *keys, uint64_t *bounds);
+
 /* ---- synthetic inputs generated in HBM (benchmarks; seeded, deterministic) */
 /* Reference-mode snapshots per SURVEY.md §8(d) C1/C3. */
 int nas_synth_snapshots(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t n_snapshots);

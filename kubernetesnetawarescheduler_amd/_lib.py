@@ -81,6 +81,8 @@ SIGNATURES = {
     "nas_get_candidates": (_I, [_CTX, _V, _V, _V, _V, _V]),
     "nas_comm_unique_id": (_I, [_V]),
     "nas_comm_init": (_I, [_CTX, _V, _I, _I]),
+    "nas_set_shard": (_I, [_CTX, _I, _I]),
+    "nas_get_candidate_keys": (_I, [_CTX, _V, _V]),
     "nas_synth_snapshots": (_I, [_CTX, _c.c_uint64, _I, _I]),
     "nas_read_snapshot": (_I, [_CTX, _I, _V, _V, _V, _V, _V, _V]),
     "nas_synth_cluster": (_I, [_CTX, _c.c_uint64, _I, _I, _I, _I]),

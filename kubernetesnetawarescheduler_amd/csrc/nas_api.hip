@@ -199,7 +199,7 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
                             (int64_t)ctx->Pp * KC, ctx->Pp, 0, p_lo, p_hi - p_lo,
                             ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>()));
-    if (ctx->world > 1) {
+    if (ctx->world > 1 && !ctx->virtual_shard) {
         // exchange the per-shard lists of pods [pr0, pr1) and merge across ranks
         auto comm = reinterpret_cast<ncclComm_t>(ctx->comm);
         ncclResult_t r = ncclGroupStart();
@@ -236,7 +236,7 @@ int alloc_extended(nas_ctx *ctx) {
     OK(nas::ensure(ctx, ctx->out_cost_i, (size_t)ctx->Pp * 4));
     OK(nas::ensure(ctx, ctx->status, 256));
     OK(nas::ensure(ctx, ctx->cap_snap, (size_t)3 * ctx->N * 4));
-    if (ctx->world > 1) {
+    if (ctx->world > 1 && !ctx->virtual_shard) {
         OK(nas::ensure(ctx, ctx->gather, (size_t)ctx->world * ctx->Pp * KC * 8));
         OK(nas::ensure(ctx, ctx->gbound, (size_t)ctx->world * ctx->Pp * 8));
     }
@@ -594,6 +594,9 @@ int nas_score(nas_ctx *ctx) {
 int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_score_out) {
     OK(bind(ctx));
     OK(check_extended(ctx));
+    if (ctx->virtual_shard)
+        return nas::fail(ctx, NAS_ERR_STATE,
+                         "nas_place on a shard needs nas_comm_init (nas_set_shard scores only)");
     if (!node_out) return nas::fail(ctx, NAS_ERR_ARG, "node_out null");
     OK(alloc_extended(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
@@ -726,6 +729,7 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     }
     ctx->rank = rank;
     ctx->world = world;
+    ctx->virtual_shard = false;
     if (world == 1) return NAS_OK;
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
@@ -734,6 +738,32 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     if (r != ncclSuccess)
         return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     ctx->comm = reinterpret_cast<ncclComm *>(comm);
+    return NAS_OK;
+}
+
+int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world) {
+    OK(bind(ctx));
+    if (world < 1 || rank < 0 || rank >= world)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_set_shard: rank/world");
+    if (ctx->comm) return nas::fail(ctx, NAS_ERR_STATE, "context already has a communicator");
+    if (ctx->have_L || ctx->have_wa || ctx->have_cap)
+        return nas::fail(ctx, NAS_ERR_STATE, "nas_set_shard must precede the extended uploads");
+    ctx->rank = rank;
+    ctx->world = world;
+    ctx->virtual_shard = world > 1;
+    return NAS_OK;
+}
+
+int nas_get_candidate_keys(nas_ctx *ctx, uint64_t *keys, uint64_t *bounds) {
+    OK(bind(ctx));
+    if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
+    if (keys)
+        HIPCK(hipMemcpyAsync(keys, ctx->cand_key.p, (size_t)ctx->P * KC * 8, hipMemcpyDeviceToHost,
+                             ctx->stream));
+    if (bounds)
+        HIPCK(hipMemcpyAsync(bounds, ctx->cand_bound.p, (size_t)ctx->P * 8, hipMemcpyDeviceToHost,
+                             ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
     return NAS_OK;
 }
 

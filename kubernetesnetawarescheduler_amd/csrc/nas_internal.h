@@ -90,6 +90,7 @@ struct nas_ctx {
     // ---- multi-GPU
     ncclComm *comm = nullptr;
     int32_t rank = 0, world = 1;
+    bool virtual_shard = false;  // nas_set_shard: shard geometry, no exchange
 };
 
 namespace nas {

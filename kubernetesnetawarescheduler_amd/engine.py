@@ -105,6 +105,15 @@ class Engine:
         b = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
         self._ck(self._L.nas_comm_init(self._h, b, rank, world))
 
+    def set_shard(self, rank, world):
+        self._ck(self._L.nas_set_shard(self._h, rank, world))
+
+    def candidate_keys(self):
+        keys = np.empty((self.n_pods, _lib.K_CANDIDATES), np.uint64)
+        bounds = np.empty(self.n_pods, np.uint64)
+        self._ck(self._L.nas_get_candidate_keys(self._h, ptr(keys), ptr(bounds)))
+        return keys, bounds
+
     @staticmethod
     def comm_unique_id():
         b = (ctypes.c_uint8 * 128)()

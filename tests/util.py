@@ -41,3 +41,29 @@ def cluster(rng, P, N, dtype="i8", lo=0, hi=20, cap_scale=1.0, int_valued=True):
 
 def all_perms(n):
     return np.array(list(itertools.permutations(range(n))), np.int32)
+
+
+KEY_INVALID = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def keys_from_costs(nodes, costs):
+    """int costs (< 2^31 in magnitude) + node ids -> packed keys (cost ^ 2^31) << 32 | node."""
+    nodes = np.asarray(nodes)
+    k = ((np.asarray(costs).astype(np.int64) ^ np.int64(-2**31)) & 0xFFFFFFFF).astype(np.uint64)
+    k = (k << np.uint64(32)) | (nodes.astype(np.int64) & 0xFFFFFFFF).astype(np.uint64)
+    return np.where(nodes >= 0, k, KEY_INVALID)
+
+
+def merge_lists(parts, K=8):
+    """Merge per-shard candidate lists [(keys (P,K), bounds (P,)), ...] with the
+    engine's rule: keep the K smallest keys, bound = min(bounds, kept[K-1])."""
+    keys = np.sort(np.concatenate([k for k, _ in parts], axis=1), axis=1)[:, :K]
+    bound = np.minimum.reduce([b for _, b in parts] + [keys[:, K - 1]])
+    return keys, bound
+
+
+def usable(keys, bound):
+    """Exact prefix of each list: node ids and count."""
+    ok = (keys != KEY_INVALID) & (keys <= bound[:, None])
+    nodes = np.where(ok, (keys & np.uint64(0xFFFFFFFF)).astype(np.int64), -1).astype(np.int32)
+    return nodes, ok.sum(axis=1).astype(np.int32)
