@@ -31,9 +31,12 @@ PEAK_I8_TOPS = 5033.2     # dense int8 MFMA, 256 CU x 4 SIMD x 2048 op/clk x 2.4
 PEAK_BF16_TFLOPS = 2516.6  # dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # HBM3E spec (MI355X_MICROARCH.md)
 SEED = 0x4E4153
-# HBM bytes per k_cost_topk launch from rocprofv3 PMC passes (profiles/, see
-# DESIGN.md): (FETCH_SIZE x 2 gfx950 correction + WRITE_SIZE) in bytes, or None
-PMC_TRAFFIC = {}
+# HBM-side bytes per launch from rocprofv3 PMC passes (tools/prof_bench.sh ->
+# profiles/r01_prof_summary.json): FETCH_SIZE x 2 (gfx950 correction,
+# MI355X_MICROARCH.md) + WRITE_SIZE, for the default workload on one GPU only;
+# any other (kernel, dtype, nodes, pods, world) reports null.
+PMC_TRAFFIC = {("k_cost_topk", "i8", 10000, 100000, 1): 16785070208.0,
+               ("k_vote", "i8", 10000, 100000, 1): 48088185536.0}
 
 
 def parse():
@@ -47,7 +50,7 @@ def parse():
     ap.add_argument("--peers", type=int, default=8)
     ap.add_argument("--no-reference-mode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=12.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--only", choices=["place", "vote", "score"], default=None,
                     help="profile helper: run only one path")
     return ap.parse_args()
@@ -185,7 +188,7 @@ def cpu_baseline_place(args, eng, gpu_nodes):
         dt = time.perf_counter() - t0
         spent += dt
         t_total, pods_done, placements = dt, Ps, node
-        if spent > args.cpu_budget_s / 3 or Ps >= 4096:
+        if dt > args.cpu_budget_s / 2 or Ps >= 16384:
             break
         Ps *= 2
     match = bool((gpu_nodes[:pods_done] == placements).all())
@@ -204,7 +207,7 @@ def cpu_baseline_vote(args, eng, ref):
     import oracle
     o1, o2, best, win = ref
     N = args.nodes
-    snaps, idx = [], list(range(0, min(eng.snap_count, 4000), 7))
+    snaps, idx = [], list(range(0, eng.snap_count, 3))
     t_total, done, ok = 0.0, 0, True
     for s in idx:
         snap = eng.read_snapshot(s)
@@ -213,7 +216,7 @@ def cpu_baseline_vote(args, eng, ref):
         t_total += time.perf_counter() - t0
         done += 1
         ok &= (b == best[s]) and (list(w) == win[s].tolist())
-        if t_total > args.cpu_budget_s / 6:
+        if t_total > args.cpu_budget_s / 2:
             break
     return {"value": done * N / t_total, "unit": "pair-scores/s", "cores": 1, "kind": "port",
             "sample": f"oracle or_vote_literal (C restatement of scheduler.go:250-394, one "
@@ -259,11 +262,12 @@ def main():
         peak = PEAK_I8_TOPS if args.dtype == "i8" else PEAK_BF16_TFLOPS
         out["roofline"] = {"kernel": "k_cost_topk", "bound": "mfma", "achieved": achieved,
                            "peak": peak, "unit": "TOPS" if args.dtype == "i8" else "TFLOP/s",
-                           "frac": achieved / peak, "traffic": PMC_TRAFFIC.get(args.dtype),
+                           "frac": achieved / peak, "traffic": PMC_TRAFFIC.get(("k_cost_topk", args.dtype, N, P, d.world)),
+                           "traffic_unit": "B/launch",
                            "launch_ms": cost_ms, "ops_per_launch": ops,
                            "note": "one launch over all pods x this rank's node columns "
                                    "(nas_score), HIP events on its stream; 2*P*N*N_local ops"}
-    if not args.no_reference_mode and args.only != "place":
+    if not args.no_reference_mode and args.only in (None, "vote"):
         elapsed, vote_ms, S, ref = bench_vote(args, d, eng)
         bytes_launch = 48.0 * N * S
         out["reference_mode"] = {
@@ -274,7 +278,8 @@ def main():
                          "achieved": bytes_launch / (vote_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s",
                          "frac": bytes_launch / (vote_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                         "traffic": None, "launch_ms": vote_ms, "bytes_per_launch": bytes_launch}}
+                         "traffic": PMC_TRAFFIC.get(("k_vote", args.dtype, N, P, d.world)),
+                         "traffic_unit": "B/launch", "launch_ms": vote_ms, "bytes_per_launch": bytes_launch}}
         if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
             out["reference_mode"]["cpu_baseline"] = cpu_baseline_vote(args, eng, ref)
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and gpu_nodes is not None:
