@@ -11,27 +11,50 @@
 // means no node fits (NAS_EMPTY); otherwise the pod needs a rescore against
 // the current capacity (host loop in nas_api.hip).
 //
-// Parallel form: one wave64 takes 64 consecutive pods (a chunk).  Every
-// not-yet-committed lane picks its first fitting usable candidate against the
-// current capacity.  Lanes whose picks are pairwise distinct are independent
-// of one another, so the prefix of lanes before the first repeated pick
-// (detected with an LDS atomicMin bucket table; a hash collision only
-// shortens the prefix) is committed at once -- exactly what the sequential
-// walk does -- and the remaining lanes of the same chunk pick again against
-// the updated capacity.  Chunks stay aligned, so the next ones are prefetched
-// RING chunks ahead into a statically indexed register ring, hiding the
-// global-load latency behind the walk.
-// The working capacity lives in LDS (3 x N int32) when it fits, else in L2;
-// the whole workgroup copies it in and out, one wave runs the walk.
+// Parallel form: one 1024-thread workgroup, one pod per thread, a window of
+// 1024 consecutive pods per round.
+//   1. Every pending pod picks its first fitting usable candidate against the
+//      capacity at the start of the round and RESERVES it with per-resource
+//      compare-and-swap loops that never take a resource below zero (so no
+//      overflow, whatever the request sizes).
+//   2. A pod is BAD if a reservation failed or it needs a rescore; s = the
+//      lowest bad pod (LDS atomicMin).
+//   3. Every pod below s is exactly what the sequential walk does: for the
+//      pods below s on any node c, the last of them to reserve (in atomic
+//      order) still found its request available after all the others that
+//      reserved before it, so their total fits c, hence every prefix of them
+//      in pod order does; and nothing below s changed its mind.  They commit.
+//   4. Pods >= s release their reservations.  Pod s re-checks its pick
+//      against the capacity now (= start minus the committed pods): if it
+//      fits it commits too.  The round ends; the next one re-runs the same
+//      window with the pods not yet committed (the first of them always
+//      commits, so every round makes progress).
+// A round with no bad pod costs one barrier; the next window's lists are
+// prefetched into registers while the current one runs.  A rescore pod
+// halts the launch (halt word) after the pods below it commit.
+// The working capacity lives in LDS (3 x N int32) when it fits, else in L2.
 #include "klist.h"
 
 namespace nas {
 namespace {
 
-constexpr int THREADS = 256;  // 4 waves copy the capacity in and out; wave 0 walks
-constexpr int HBUCKETS = 4096;
-constexpr int FREE_SLOT = 0x7fffffff;
-constexpr int LDS_CAP_MAX_NODES = (160 * 1024 - HBUCKETS * 4 - 64) / 12;
+constexpr int THREADS = 1024;  // one window of pods per round
+constexpr int LDS_DYN_MAX = 160 * 1024 - 512;  // leaves room for the static LDS
+constexpr int LDS_CAP_MAX_NODES = LDS_DYN_MAX / 12;
+constexpr int NO_POD = 0x7fffffff;
+
+// reserve r from *c iff *c >= r, never going below zero; returns success
+template <bool LDS_CAP>
+__device__ __forceinline__ bool reserve(int *c, int r) {
+    if (r == 0) return true;
+    int old = LDS_CAP ? *c : __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (old >= r) {
+        const int prev = atomicCAS(c, old, old - r);
+        if (prev == old) return true;
+        old = prev;
+    }
+    return false;
+}
 
 template <bool LDS_CAP>
 __global__ void __launch_bounds__(THREADS)
@@ -40,120 +63,136 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
          int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
          int *__restrict__ halt) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
-    int *table = smem;
-    int *capl = smem + HBUCKETS;
+    __shared__ int first_bad[3];  // round r uses slot r % 3
+    int *capl = smem;
     const int tid = threadIdx.x;
     // an earlier commit launch on this stream stopped at a pod that needs a
     // rescore: every later pod must wait for it (sequential semantics)
     if (__hip_atomic_load(halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0) return;
-    for (int i = tid; i < HBUCKETS; i += THREADS) table[i] = FREE_SLOT;
     if (LDS_CAP)
         for (int i = tid; i < 3 * N; i += THREADS) capl[i] = cap_g[i];
     int *cap = LDS_CAP ? capl : cap_g;
-    __syncthreads();
+    if (tid == 0) first_bad[0] = first_bad[1] = first_bad[2] = NO_POD;
 
-    if (tid < 64) {
-        const int lane = tid;
-        auto ld = [&](int idx) -> int {
-            if (LDS_CAP) return cap[idx];
-            return __hip_atomic_load(cap + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        };
-        struct Chunk {
-            u64 k[KC];
-            u64 bound;
-            int r0, r1, r2;
-        };
-        // branch-free (a branchy fill kept Chunk fields in scratch): lanes
-        // past p_end read a clamped, in-bounds pod and mark it inactive
-        auto load = [&](int base, Chunk &c) {
-            const int i = base + lane;
-            const bool ok = i < p_end;
-            const int ii = min(i, Pp - 1);
-            load8(cand_key + (size_t)ii * KC, c.k);
-            const u64 b = cand_bound[ii];
-            const int r0 = req[ii], r1 = req[Pp + ii], r2 = req[2 * Pp + ii];
+    struct Pod {
+        u64 k[KC];
+        u64 bound;
+        int r0, r1, r2;
+    };
+    // branch-free fill: pods past p_end read a clamped, in-bounds row and are
+    // marked inactive (no usable key, complete list)
+    auto load = [&](int base, Pod &c) {
+        const int i = base + tid;
+        const bool ok = i < p_end;
+        const int ii = min(i, Pp - 1);
+        load8(cand_key + (size_t)ii * KC, c.k);
+        const u64 b = cand_bound[ii];
+        const int r0 = req[ii], r1 = req[Pp + ii], r2 = req[2 * Pp + ii];
 #pragma unroll
-            for (int j = 0; j < KC; ++j) c.k[j] = ok ? c.k[j] : KEY_INVALID;
-            c.bound = ok ? b : KEY_INVALID;
-            c.r0 = ok ? r0 : 0;
-            c.r1 = ok ? r1 : 0;
-            c.r2 = ok ? r2 : 0;
-        };
-        // walk one chunk to completion; returns the pod that needs a rescore,
-        // or -1 when every lane of the chunk is committed
-        auto walk = [&](const Chunk &cur, int base) -> int {
-            bool done = base + lane >= p_end;
-            while (true) {
-                bool fit[KC];
+        for (int j = 0; j < KC; ++j) c.k[j] = ok ? c.k[j] : KEY_INVALID;
+        c.bound = ok ? b : KEY_INVALID;
+        c.r0 = r0;
+        c.r1 = r1;
+        c.r2 = r2;
+    };
+    auto ld = [&](int idx) -> int {
+        if (LDS_CAP) return cap[idx];
+        return __hip_atomic_load(cap + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+
+    Pod cur, nxt;
+    load(p_begin, cur);
+    __syncthreads();
+    int round = 0;
+    int stop = p_end;
+    for (int base = p_begin; base < p_end; base += THREADS) {
+        if (base + THREADS < p_end) load(base + THREADS, nxt);  // prefetch the next window
+        const int i = base + tid;
+        bool done = i >= p_end;
+        while (true) {
+            // slot (round + 1) % 3 was last read before the previous round's
+            // first barrier and is next written after this round's: reset it
+            if (tid == 0) first_bad[(round + 1) % 3] = NO_POD;
+            // 1. pick against the capacity at the start of the round, reserve
+            bool fit[KC];
 #pragma unroll
-                for (int j = 0; j < KC; ++j) {
-                    const bool usable = cur.k[j] != KEY_INVALID && cur.k[j] <= cur.bound;
-                    const int n = usable ? (int)(unsigned)cur.k[j] : 0;
-                    const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
-                    fit[j] = usable && cur.r0 <= a && cur.r1 <= b && cur.r2 <= c;
+            for (int j = 0; j < KC; ++j) {
+                const bool usable = cur.k[j] != KEY_INVALID && cur.k[j] <= cur.bound;
+                const int n = usable ? (int)(unsigned)cur.k[j] : 0;
+                const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
+                fit[j] = usable && cur.r0 <= a && cur.r1 <= b && cur.r2 <= c;
+            }
+            int choice = -1;
+            unsigned ccost = 0;
+#pragma unroll
+            for (int j = KC - 1; j >= 0; --j) {
+                if (fit[j]) {
+                    choice = (int)(unsigned)cur.k[j];
+                    ccost = (unsigned)(cur.k[j] >> 32);
                 }
-                int choice = -1;
-                unsigned ccost = 0;
-#pragma unroll
-                for (int j = KC - 1; j >= 0; --j) {
-                    if (fit[j]) {
-                        choice = (int)(unsigned)cur.k[j];
-                        ccost = (unsigned)(cur.k[j] >> 32);
-                    }
-                }
-                if (done) choice = -1;
-                const bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
-                // repeated picks: the lowest lane per bucket wins (one wave:
-                // LDS operations complete in issue order, no barrier needed)
-                const int h = choice & (HBUCKETS - 1);
-                if (choice >= 0) atomicMin(&table[h], lane);
-                const bool dup = choice >= 0 && table[h] != lane;
-                if (choice >= 0) table[h] = FREE_SLOT;
-                const u64 bad = __ballot(rescore || dup);
-                const int f = bad ? __ffsll((long long)bad) - 1 : 64;
-                if (!done && lane < f) {
-                    const int i = base + lane;
-                    if (choice >= 0) {
-                        // picks of lanes < f are pairwise distinct: plain updates
-                        if (LDS_CAP) {
-                            cap[choice] -= cur.r0; cap[N + choice] -= cur.r1;
-                            cap[2 * N + choice] -= cur.r2;
-                        } else {
-                            atomicSub(cap + choice, cur.r0); atomicSub(cap + N + choice, cur.r1);
-                            atomicSub(cap + 2 * N + choice, cur.r2);
-                        }
-                    }
+            }
+            if (done) choice = -1;
+            const bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
+            bool g0 = false, g1 = false, g2 = false;
+            if (choice >= 0) {
+                g0 = reserve<LDS_CAP>(cap + choice, cur.r0);
+                g1 = reserve<LDS_CAP>(cap + N + choice, cur.r1);
+                g2 = reserve<LDS_CAP>(cap + 2 * N + choice, cur.r2);
+            }
+            const bool bad = rescore || (choice >= 0 && !(g0 && g1 && g2));
+            int *fb = &first_bad[round % 3];
+            if (bad) atomicMin(fb, i);
+            __syncthreads();
+            // 2. the lowest bad pod
+            const int s = *fb;
+            ++round;
+            if (s == NO_POD) {
+                // 3. no conflict: every pending pod of the window commits
+                if (!done) {
                     out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
+                    out_cost[i] = ccost;
+                }
+                break;
+            }
+            // 4. pods >= s release what they reserved; pods < s commit
+            if (!done && i >= s && choice >= 0) {
+                if (g0) atomicAdd(cap + choice, cur.r0);
+                if (g1) atomicAdd(cap + N + choice, cur.r1);
+                if (g2) atomicAdd(cap + 2 * N + choice, cur.r2);
+            }
+            if (!done && i < s) {
+                out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
+                out_cost[i] = ccost;
+                done = true;
+            }
+            __syncthreads();
+            if (i == s && !rescore) {
+                // pod s against the capacity left by the pods below it
+                const int n = choice;
+                if (cur.r0 <= ld(n) && cur.r1 <= ld(N + n) && cur.r2 <= ld(2 * N + n)) {
+                    if (LDS_CAP) {
+                        cap[n] -= cur.r0; cap[N + n] -= cur.r1; cap[2 * N + n] -= cur.r2;
+                    } else {
+                        atomicSub(cap + n, cur.r0); atomicSub(cap + N + n, cur.r1);
+                        atomicSub(cap + 2 * N + n, cur.r2);
+                    }
+                    out_node[i] = n;
                     out_cost[i] = ccost;
                     done = true;
                 }
-                if (f < 64 && ((__ballot(rescore) >> f) & 1ull)) return base + f;
-                if (__ballot(!done) == 0) return -1;
             }
-        };
-
-        constexpr int RING = 6;
-        Chunk ring[RING];
-#pragma unroll
-        for (int s = 0; s < RING; ++s) load(p_begin + 64 * s, ring[s]);
-        int stop = p_end;
-        int base = p_begin;
-        while (base < p_end && stop == p_end) {
-#pragma unroll
-            for (int s = 0; s < RING; ++s) {  // static slot index: the ring stays in VGPRs
-                if (base < p_end && stop == p_end) {
-                    const int r = walk(ring[s], base);
-                    if (r >= 0) {
-                        stop = r;
-                    } else {
-                        load(base + 64 * RING, ring[s]);
-                        base += 64;
-                    }
-                }
+            const bool halted = s >= base && s < base + THREADS && s == i && rescore;
+            // a rescore pod ends the launch: everything below it is committed
+            if (__syncthreads_or(halted)) {
+                stop = s;
+                break;
             }
+            // pods below s are done; s itself is done unless it must re-pick
         }
-        if (lane == 0 && stop < p_end) *halt = stop;
+        if (stop < p_end) break;
+        if (base + THREADS < p_end) cur = nxt;
     }
+    if (tid == 0 && stop < p_end) *halt = stop;
     __syncthreads();
     if (LDS_CAP)
         for (int i = tid; i < 3 * N; i += THREADS) cap_g[i] = capl[i];
@@ -164,24 +203,25 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost, int32_t *halt) {
+    if (p_end <= p_begin) return hipSuccess;
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
     if (N <= LDS_CAP_MAX_NODES) {
-        const size_t lds = (HBUCKETS + 3 * (size_t)N) * 4;
+        const size_t lds = 3 * (size_t)N * 4;
         static bool attr = false;
         if (!attr) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_commit<true>),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               160 * 1024);
+                                               LDS_DYN_MAX);
             if (e != hipSuccess) return e;
             attr = true;
         }
         k_commit<true><<<1, THREADS, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
                                                 oc, halt);
     } else {
-        k_commit<false><<<1, THREADS, HBUCKETS * 4, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
-                                                          out_node, oc, halt);
+        k_commit<false><<<1, THREADS, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
+                                               oc, halt);
     }
     return hipGetLastError();
 }

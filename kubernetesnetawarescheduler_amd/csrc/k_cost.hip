@@ -421,24 +421,44 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 }
 
 // merge n_lists candidate lists per pod (list l of pod p at
-// keys[l * stride + (p - src_p0) * KC], bound[l * bstride + p - src_p0])
-__global__ void k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_lists,
-                        long long stride, long long bstride, int src_p0, int p0, int np,
-                        u64 *__restrict__ dst, u64 *__restrict__ dst_bound) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= np) return;
-    const int p = p0 + i;
-    const size_t ps = (size_t)(p - src_p0);
+// keys[l * stride + (p - src_p0) * KC], bound[l * bstride + p - src_p0]).
+// MERGE_LANES lanes per pod: lane s folds lists s, s + MERGE_LANES, ... in
+// registers, then three xor-shuffle rounds merge the lanes' lists.  The 8
+// smallest keys of the union do not depend on the merge tree, and neither
+// does the bound: every intermediate kept[7] is >= the final kept[7], so the
+// result is min(all list bounds, final kept[7]) -- identical to a serial fold.
+constexpr int MERGE_LANES = 8;
+
+__global__ void __launch_bounds__(256)
+k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_lists,
+        long long stride, long long bstride, int src_p0, int p0, int np,
+        u64 *__restrict__ dst, u64 *__restrict__ dst_bound) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = t / MERGE_LANES, s = t % MERGE_LANES;
+    const bool live = i < np;  // the whole 8-lane group shares i: shuffles stay in-group
+    const size_t ps = (size_t)(p0 + (live ? i : 0) - src_p0);
     u64 a[8], bb[8];
-    load8(keys + ps * KC, a);
-    u64 bound = bounds[ps];
-    for (int l = 1; l < n_lists; ++l) {
-        load8(keys + l * stride + ps * KC, bb);
-        merge88(a, bb);
-        bound = umin64(umin64(bound, bounds[l * bstride + ps]), a[7]);
+    u64 bound = KEY_INVALID;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = KEY_INVALID;
+    if (live) {
+        for (int l = s; l < n_lists; l += MERGE_LANES) {
+            load8(keys + l * stride + ps * KC, bb);
+            merge88(a, bb);
+            bound = umin64(bound, bounds[l * bstride + ps]);
+        }
     }
+#pragma unroll
+    for (int m = 1; m < MERGE_LANES; m <<= 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bb[j] = shfl_xor64(a[j], m);
+        bound = umin64(bound, shfl_xor64(bound, m));
+        merge88(a, bb);
+    }
+    if (!live || s != 0) return;
+    const int p = p0 + i;
     store8(dst + (size_t)p * KC, a);
-    dst_bound[p] = bound;
+    dst_bound[p] = umin64(bound, a[7]);
 }
 
 #ifdef NAS_DIAG_VARIANTS
@@ -494,7 +514,7 @@ hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bo
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound) {
     if (np <= 0) return hipSuccess;
-    k_merge<<<(np + 255) / 256, 256, 0, st>>>(
+    k_merge<<<(int)(((int64_t)np * MERGE_LANES + 255) / 256), 256, 0, st>>>(
         reinterpret_cast<const u64 *>(keys), reinterpret_cast<const u64 *>(bounds), n_lists, stride,
         bstride, src_p0, p0, np, reinterpret_cast<u64 *>(cand_key),
         reinterpret_cast<u64 *>(cand_bound));

@@ -5,55 +5,65 @@
 // Kubernetes NodeResourcesFit rule: pod p fits node n iff
 // req[r][p] <= free[r][n] for r in {cpu millicores, memory KiB, pod slots}.
 //
-// Layout: lane-per-node.  Each wave owns a 64-node chunk and keeps that
-// chunk's free capacity in VGPRs (one coalesced SoA read); it then walks the
-// pods 64 at a time: one coalesced load of their requests, broadcast to the
-// wave with v_readlane, and the three vector compares produce the 64-bit fit
-// mask of (pod, chunk) directly in an SGPR pair (a ballot).  64 consecutive pods' masks are collected one per lane and
-// written with one coalesced 8-byte-per-lane store:
+// Layout: lane-per-pod.  A block owns 256 consecutive pods (one per lane;
+// requests in VGPRs, one coalesced read) and FIT_CHUNKS 64-node chunks, whose
+// capacities it stages once in LDS (SoA, padding nodes = -1 so they never
+// fit).  Per node, the wave reads the node's three capacities with
+// wave-uniform (broadcast) ds_read_b128s, three v_cmp give the fit lane mask
+// and one shift-and-add folds it into the lane's 32-bit word (nodes visited
+// high to low, so bit j ends up as node j).  Every lane then holds its pod's
+// 64-bit word for the chunk and the wave writes them with one coalesced
+// 8-byte-per-lane store:
 //   mask[c * Pp + p]  bit j  <=>  pod p fits local node 64c + j.
-// HBM-bound on the mask write (P*N/8 bytes) -- see DESIGN.md.
+// ~5 VALU per 64 pairs: the kernel runs near the speed of its mask write
+// (P*N/8 bytes, HBM) -- see DESIGN.md.
 #include "nas_internal.h"
 
 namespace nas {
 namespace {
 
-constexpr int FIT_THREADS = 256;       // 4 waves = 4 node chunks per block
-constexpr int FIT_PODS_PER_BLOCK = 512;
+constexpr int FIT_THREADS = 256;  // 4 waves = 256 pods per block
+constexpr int FIT_CHUNKS = 8;     // 512 nodes per block
+
+typedef int v4i __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(FIT_THREADS)
 k_fit(const int *__restrict__ cap, int N, int n0, int nloc, int n_chunks,
       const int *__restrict__ req, int Pp, int p0, int p_end, unsigned long long *__restrict__ mask) {
-    const int lane = threadIdx.x & 63;
-    const int c = blockIdx.y * (FIT_THREADS / 64) + (threadIdx.x >> 6);
-    if (c >= n_chunks) return;  // wave-uniform
-    const int nl = c * 64 + lane;  // local node
-    // padding nodes (nl >= nloc) never fit: requests are >= 0
-    int fc = -1, fm = -1, fp = -1;
-    if (nl < nloc) {
-        fc = cap[n0 + nl];
-        fm = cap[N + n0 + nl];
-        fp = cap[2 * N + n0 + nl];
-    }
-    const int *rc = req, *rm = req + Pp, *rp = req + 2 * Pp;
-    const int pb = p0 + blockIdx.x * FIT_PODS_PER_BLOCK;
-    const int pe = min(p_end, pb + FIT_PODS_PER_BLOCK);
-    for (int p = pb; p < pe; p += 64) {
-        // one coalesced load of 64 pods' requests, broadcast with v_readlane
-        const int q = p + lane;
-        const int a = q < pe ? rc[q] : 0x7fffffff;
-        const int b = q < pe ? rm[q] : 0x7fffffff;
-        const int d = q < pe ? rp[q] : 0x7fffffff;
-        unsigned long long mine = 0;
+    __shared__ __attribute__((aligned(16))) int sc[3][FIT_CHUNKS * 64];
+    const int tid = threadIdx.x;
+    const int c0 = blockIdx.y * FIT_CHUNKS;
+    const int c1 = min(n_chunks, c0 + FIT_CHUNKS);
+    for (int i = tid; i < FIT_CHUNKS * 64; i += FIT_THREADS) {
+        const int nl = c0 * 64 + i;
+        const bool real = nl < nloc;
 #pragma unroll
-        for (int i = 0; i < 64; ++i) {
-            const int ra = __builtin_amdgcn_readlane(a, i);
-            const int rb = __builtin_amdgcn_readlane(b, i);
-            const int rd = __builtin_amdgcn_readlane(d, i);
-            const unsigned long long m = __ballot(ra <= fc && rb <= fm && rd <= fp);
-            mine = lane == i ? m : mine;
+        for (int r = 0; r < 3; ++r) sc[r][i] = real ? cap[(size_t)r * N + n0 + nl] : -1;
+    }
+    const int p = p0 + blockIdx.x * FIT_THREADS + tid;
+    const int q = min(p, Pp - 1);
+    const int ra = req[q], rb = req[Pp + q], rd = req[2 * Pp + q];
+    __syncthreads();
+    for (int c = c0; c < c1; ++c) {
+        const int *lc = &sc[0][(c - c0) * 64], *lm = &sc[1][(c - c0) * 64];
+        const int *lp = &sc[2][(c - c0) * 64];
+        unsigned w[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            unsigned acc = 0;
+#pragma unroll
+            for (int j4 = 7; j4 >= 0; --j4) {
+                const int o = h * 32 + j4 * 4;
+                const v4i fc = *reinterpret_cast<const v4i *>(lc + o);
+                const v4i fm = *reinterpret_cast<const v4i *>(lm + o);
+                const v4i fp = *reinterpret_cast<const v4i *>(lp + o);
+#pragma unroll
+                for (int j = 3; j >= 0; --j)
+                    acc = acc * 2u + ((ra <= fc[j] && rb <= fm[j] && rd <= fp[j]) ? 1u : 0u);
+            }
+            w[h] = acc;
         }
-        if (q < pe) mask[(size_t)c * Pp + q] = mine;
+        if (p < p_end) mask[(size_t)c * Pp + p] = ((unsigned long long)w[1] << 32) | w[0];
     }
 }
 
@@ -64,8 +74,8 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
     (void)P;
     if (np <= 0) return hipSuccess;
     const int n_chunks = Mp / 64;
-    dim3 grid((np + FIT_PODS_PER_BLOCK - 1) / FIT_PODS_PER_BLOCK,
-              (n_chunks + FIT_THREADS / 64 - 1) / (FIT_THREADS / 64));
+    dim3 grid((np + FIT_THREADS - 1) / FIT_THREADS,
+              (n_chunks + FIT_CHUNKS - 1) / FIT_CHUNKS);
     k_fit<<<grid, FIT_THREADS, 0, st>>>(cap, N, n0, nloc, n_chunks, req, Pp, p0, p0 + np,
                                         reinterpret_cast<unsigned long long *>(mask));
     return hipGetLastError();

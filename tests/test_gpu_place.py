@@ -206,3 +206,42 @@ def test_synthetic_cluster_sampled(engine):
         assert (engine.get_capacity() == wfree).all()
     else:  # the GPU rescored from `stop` on: the prefix before it must agree
         assert placed[:stop].tolist() == want[:stop].tolist()
+
+
+@pytest.mark.parametrize("P,N,seed", [(6000, 64, 1), (10000, 300, 2), (3000, 1000, 3)])
+def test_commit_conflicts_exact(engine, P, N, seed):
+    """Crowded commit windows: most pods of a 1024-pod window want the same
+    few nodes, which fill up mid-window (reservation failures, releases,
+    re-picks) -- placements and remaining capacity equal the sequential oracle."""
+    rng = np.random.default_rng(seed)
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=40, cap_scale=0.2)
+    hot = rng.choice(N, max(2, N // 32), replace=False)
+    WA[:, hot] = 127
+    L[hot[:, None], hot[None, :]] = 0
+    upload(engine, WA, L, free, req, "i8")
+    node, _, ci = engine.place()
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    assert node.tolist() == want.tolist()
+    assert ci.tolist() == wcost.tolist()
+    assert (engine.get_capacity() == wfree).all()
+
+
+def test_commit_huge_requests_no_overflow(engine):
+    """Requests near 2^30 against capacities near 2^31: a window's combined
+    reservations would overflow int32; the commit never takes a resource
+    below zero, so placements stay exact."""
+    rng = np.random.default_rng(4)
+    P, N = 3000, 40
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=20)
+    free[:, 0] = rng.integers(2**31 - 2**28, 2**31 - 1, N)
+    free[:, 1] = 2**31 - 1
+    free[:, 2] = 2**31 - 1
+    req[:, 0] = rng.integers(2**29, 2**30, P)
+    req[:, 1] = rng.integers(2**29, 2**30, P)
+    upload(engine, WA, L, free, req, "i8")
+    node, _, ci = engine.place()
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    assert node.tolist() == want.tolist()
+    assert ci.tolist() == wcost.tolist()
+    assert (engine.get_capacity() == wfree).all()
+    assert (want < 0).sum() > 0  # the cluster overflows: unschedulable pods exist
