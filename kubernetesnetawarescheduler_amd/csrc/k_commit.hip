@@ -29,9 +29,10 @@
 //      fits it commits too.  The round ends; the next one re-runs the same
 //      window with the pods not yet committed (the first of them always
 //      commits, so every round makes progress).
-// A round with no bad pod costs one barrier; the next window's lists are
+// A round with no bad pod costs two barriers; the next window's lists are
 // prefetched into registers while the current one runs.  A rescore pod
-// halts the launch (halt word) after the pods below it commit.
+// halts the launch (halt word) after the pods below it commit; a launch with
+// p_begin < 0 resumes from the halted pod after a rescore slot (nas_api.hip).
 // The working capacity lives in LDS (3 x N int32) when it fits, else in L2.
 #include "klist.h"
 
@@ -64,11 +65,21 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
          int *__restrict__ halt) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     __shared__ int first_bad[3];  // round r uses slot r % 3
+    __shared__ int s_rescore;     // the round's lowest bad pod needs a rescore
     int *capl = smem;
     const int tid = threadIdx.x;
     // an earlier commit launch on this stream stopped at a pod that needs a
     // rescore: every later pod must wait for it (sequential semantics)
-    if (__hip_atomic_load(halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= 0) return;
+    // p_begin < 0: a rescore slot's resume -- continue from the halted pod
+    // (nothing to do unless a walk halted), clearing the halt word
+    const int h = __hip_atomic_load(halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool resume = p_begin < 0;
+    if (resume) {
+        if (h < 0) return;
+        p_begin = h;
+    } else if (h >= 0) {
+        return;
+    }
     if (LDS_CAP)
         for (int i = tid; i < 3 * N; i += THREADS) capl[i] = cap_g[i];
     int *cap = LDS_CAP ? capl : cap_g;
@@ -102,7 +113,11 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
 
     Pod cur, nxt;
     load(p_begin, cur);
-    __syncthreads();
+    __syncthreads();  // every thread has read the halt word
+    if (tid == 0 && h >= 0) {
+        halt[0] = -1;
+        if (resume) halt[1] += 1;  // device-side rescores, reported in nas_timings
+    }
     int round = 0;
     int stop = p_end;
     for (int base = p_begin; base < p_end; base += THREADS) {
@@ -133,6 +148,9 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             }
             if (done) choice = -1;
             const bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
+            // every pick must see the capacity at the START of the round: a
+            // later pod's reservation must not push an earlier pod off a node
+            __syncthreads();
             bool g0 = false, g1 = false, g2 = false;
             if (choice >= 0) {
                 g0 = reserve<LDS_CAP>(cap + choice, cur.r0);
@@ -165,8 +183,14 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 out_cost[i] = ccost;
                 done = true;
             }
+            if (i == s) s_rescore = rescore;
             __syncthreads();
-            if (i == s && !rescore) {
+            // a rescore pod ends the launch: everything below it is committed
+            if (s_rescore) {
+                stop = s;
+                break;
+            }
+            if (i == s) {
                 // pod s against the capacity left by the pods below it
                 const int n = choice;
                 if (cur.r0 <= ld(n) && cur.r1 <= ld(N + n) && cur.r2 <= ld(2 * N + n)) {
@@ -181,12 +205,9 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                     done = true;
                 }
             }
-            const bool halted = s >= base && s < base + THREADS && s == i && rescore;
-            // a rescore pod ends the launch: everything below it is committed
-            if (__syncthreads_or(halted)) {
-                stop = s;
-                break;
-            }
+            // a full barrier (with its fence): the next round's picks must see
+            // pod s's update (a bare s_barrier does not wait for the store)
+            __syncthreads();
             // pods below s are done; s itself is done unless it must re-pick
         }
         if (stop < p_end) break;
@@ -200,10 +221,12 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
 
 }  // namespace
 
+bool commit_in_lds(int N) { return N <= LDS_CAP_MAX_NODES; }
+
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost, int32_t *halt) {
-    if (p_end <= p_begin) return hipSuccess;
+    if (p_begin >= 0 && p_end <= p_begin) return hipSuccess;
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
     auto *oc = reinterpret_cast<unsigned *>(out_cost);

@@ -121,7 +121,8 @@ template <int DT, int EPI = 0, int SCHED = COST_SCHED, int PIPE = COST_PIPE, int
 __global__ void __launch_bounds__(THREADS, 1)
 k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
-            u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base) {
+            u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base,
+            const int *__restrict__ dyn_start, int dyn_hi) {
     using M = Mma<DT>;
     using acc_t = typename M::acc_t;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -137,6 +138,12 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     const int gm = min(n_mt - first_mt, GM);
     const int mt = first_mt + (v % gsize) % gm;
     const int nt = (v % gsize) / gm;
+    if (dyn_start) {  // rescore slot: pod tiles from the window start in device memory
+        const int s = *dyn_start;
+        if (s < 0) return;
+        p0 = s / BN * BN;
+        if (p0 + nt * BN >= dyn_hi) return;  // whole block: before any barrier
+    }
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w >> 2, wn = w & 3;
@@ -432,7 +439,16 @@ constexpr int MERGE_LANES = 8;
 __global__ void __launch_bounds__(256)
 k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_lists,
         long long stride, long long bstride, int src_p0, int p0, int np,
-        u64 *__restrict__ dst, u64 *__restrict__ dst_bound) {
+        u64 *__restrict__ dst, u64 *__restrict__ dst_bound, int dst_p0,
+        const int *__restrict__ dyn_start, int dyn_hi, int dyn_flags) {
+    if (dyn_start) {  // rescore slot: pods [s, min(s + np, hi)); source / destination
+        const int s = *dyn_start;  // indexed from s when flagged (window staging buffers)
+        if (s < 0) return;
+        p0 = s;
+        np = min(np, dyn_hi - s);
+        if (dyn_flags & MERGE_SRC_WINDOW) src_p0 = s;
+        if (dyn_flags & MERGE_DST_WINDOW) dst_p0 = s;
+    }
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = t / MERGE_LANES, s = t % MERGE_LANES;
     const bool live = i < np;  // the whole 8-lane group shares i: shuffles stay in-group
@@ -456,7 +472,7 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
         merge88(a, bb);
     }
     if (!live || s != 0) return;
-    const int p = p0 + i;
+    const int p = p0 + i - dst_p0;
     store8(dst + (size_t)p * KC, a);
     dst_bound[p] = umin64(bound, a[7]);
 }
@@ -465,7 +481,7 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
 #define NAS_INST(E, S, PP, G)                                                                      \
     template __global__ void k_cost_topk<NAS_DT_I8, E, S, PP, G>(                                  \
         const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
-        u64 *, int);
+        u64 *, int, const int *, int);
 NAS_INST(0, 0, 0, 4) NAS_INST(1, 0, 0, 4) NAS_INST(0, 5, 0, 4) NAS_INST(1, 5, 0, 4)
 NAS_INST(3, 5, 0, 4) NAS_INST(0, 1, 0, 4) NAS_INST(0, 5, 0, 8) NAS_INST(4, 0, 0, 4)
 #undef NAS_INST
@@ -474,7 +490,7 @@ NAS_INST(3, 5, 0, 4) NAS_INST(0, 1, 0, 4) NAS_INST(0, 5, 0, 8) NAS_INST(4, 0, 0,
 template <int DT>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,
                          int p0, int np, const uint64_t *mask, uint64_t *partial,
-                         uint64_t *pbound, int node_base) {
+                         uint64_t *pbound, int node_base, const Dyn *dyn) {
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_cost_topk<DT>),
@@ -487,7 +503,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     k_cost_topk<DT><<<n_mt * n_nt, THREADS, lds_bytes<COST_PIPE>(), st>>>(
         static_cast<const unsigned char *>(Lt), static_cast<const unsigned char *>(WA), Kb, n_mt,
         n_nt, p0, Pp, reinterpret_cast<const u64 *>(mask), reinterpret_cast<u64 *>(partial),
-        reinterpret_cast<u64 *>(pbound), node_base);
+        reinterpret_cast<u64 *>(pbound), node_base, dyn ? dyn->start : nullptr, dyn ? dyn->hi : 0);
     return hipGetLastError();
 }
 
@@ -497,27 +513,35 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
 // p0 + np <= Pp; Mp multiple of BM.
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
-                            uint64_t *partial, uint64_t *pbound, int node_base) {
+                            uint64_t *partial, uint64_t *pbound, int node_base, const Dyn *dyn) {
+    if (dyn) {  // tiles covering any window [s, s + win) clipped to hi: one extra for the offset
+        p0 = 0;
+        np = (int)round_up(dyn->win, BN) + BN;
+        if (dyn->hi > Pp) return hipErrorInvalidValue;
+    }
     if (np <= 0) return hipSuccess;
-    if (Mp % BM || np % BN || p0 + np > Pp) return hipErrorInvalidValue;
+    if (Mp % BM || np % BN || (!dyn && p0 + np > Pp)) return hipErrorInvalidValue;
     if (dtype == NAS_DT_I8) {
         if (Kp % BKB) return hipErrorInvalidValue;
         return launch_cost_t<NAS_DT_I8>(st, Lt, WA, Mp, Kp, Pp, p0, np, mask, partial, pbound,
-                                        node_base);
+                                        node_base, dyn);
     }
     if ((2 * Kp) % BKB) return hipErrorInvalidValue;
     return launch_cost_t<NAS_DT_BF16>(st, Lt, WA, Mp, 2 * Kp, Pp, p0, np, mask, partial, pbound,
-                                      node_base);
+                                      node_base, dyn);
 }
 
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
-                        uint64_t *cand_key, uint64_t *cand_bound) {
+                        uint64_t *cand_key, uint64_t *cand_bound, int dst_p0, const Dyn *dyn,
+                        int dyn_flags) {
+    if (dyn) np = dyn->win;
     if (np <= 0) return hipSuccess;
     k_merge<<<(int)(((int64_t)np * MERGE_LANES + 255) / 256), 256, 0, st>>>(
         reinterpret_cast<const u64 *>(keys), reinterpret_cast<const u64 *>(bounds), n_lists, stride,
         bstride, src_p0, p0, np, reinterpret_cast<u64 *>(cand_key),
-        reinterpret_cast<u64 *>(cand_bound));
+        reinterpret_cast<u64 *>(cand_bound), dst_p0, dyn ? dyn->start : nullptr, dyn ? dyn->hi : 0,
+        dyn_flags);
     return hipGetLastError();
 }
 

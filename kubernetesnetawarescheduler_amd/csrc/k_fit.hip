@@ -28,8 +28,15 @@ constexpr int FIT_CHUNKS = 8;     // 512 nodes per block
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(FIT_THREADS)
-k_fit(const int *__restrict__ cap, int N, int n0, int nloc, int n_chunks,
-      const int *__restrict__ req, int Pp, int p0, int p_end, unsigned long long *__restrict__ mask) {
+k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
+      const int *__restrict__ req, int Pp, int p0, int p_end, unsigned long long *__restrict__ mask,
+      const int *__restrict__ dyn_start, int dyn_win) {
+    if (dyn_start) {  // window [*dyn_start, +dyn_win) read from device memory (rescore slots)
+        const int s = *dyn_start;
+        if (s < 0) return;
+        p0 = s;
+        p_end = min(p_end, s + dyn_win);
+    }
     __shared__ __attribute__((aligned(16))) int sc[3][FIT_CHUNKS * 64];
     const int tid = threadIdx.x;
     const int c0 = blockIdx.y * FIT_CHUNKS;
@@ -37,8 +44,13 @@ k_fit(const int *__restrict__ cap, int N, int n0, int nloc, int n_chunks,
     for (int i = tid; i < FIT_CHUNKS * 64; i += FIT_THREADS) {
         const int nl = c0 * 64 + i;
         const bool real = nl < nloc;
+        // relaxed atomic loads: nas_place filters against the working
+        // capacity while the commit stream publishes into it
 #pragma unroll
-        for (int r = 0; r < 3; ++r) sc[r][i] = real ? cap[(size_t)r * N + n0 + nl] : -1;
+        for (int r = 0; r < 3; ++r)
+            sc[r][i] = real ? __hip_atomic_load(const_cast<int *>(cap) + (size_t)r * N + n0 + nl, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)
+                            : -1;
     }
     const int p = p0 + blockIdx.x * FIT_THREADS + tid;
     const int q = min(p, Pp - 1);
@@ -70,14 +82,17 @@ k_fit(const int *__restrict__ cap, int N, int n0, int nloc, int n_chunks,
 }  // namespace
 
 hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nloc, int Mp,
-                      const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask) {
+                      const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask,
+                      const Dyn *dyn) {
     (void)P;
     if (np <= 0) return hipSuccess;
     const int n_chunks = Mp / 64;
     dim3 grid((np + FIT_THREADS - 1) / FIT_THREADS,
               (n_chunks + FIT_CHUNKS - 1) / FIT_CHUNKS);
-    k_fit<<<grid, FIT_THREADS, 0, st>>>(cap, N, n0, nloc, n_chunks, req, Pp, p0, p0 + np,
-                                        reinterpret_cast<unsigned long long *>(mask));
+    k_fit<<<grid, FIT_THREADS, 0, st>>>(cap, N, n0, nloc, n_chunks, req, Pp, p0,
+                                        dyn ? dyn->hi : p0 + np,
+                                        reinterpret_cast<unsigned long long *>(mask),
+                                        dyn ? dyn->start : nullptr, dyn ? dyn->win : 0);
     return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -61,7 +62,13 @@ int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes) {
 namespace {
 
 constexpr int RESCORE_PODS = 1024;  // pods rescored per commit stop (multiple of COST_BN)
-constexpr int CHUNK_PODS = 32 * nas::COST_BN;  // pods per pipelined scoring chunk
+// Device-side rescore slots enqueued behind a chunk's commit.  An idle slot
+// still costs its launches a wait for free CUs while scoring fills the chip,
+// and scoring against the live capacity makes stops rare, so by default only
+// the last chunk (nothing left to overlap) gets slots; stops elsewhere are
+// resumed after the pipeline by the host loop.
+constexpr int RESCORE_SLOTS = 0;
+constexpr int RESCORE_SLOTS_LAST = 2;
 
 int bind(nas_ctx *ctx) {
     if (!ctx) return NAS_ERR_ARG;
@@ -177,12 +184,30 @@ int check_extended(nas_ctx *ctx) {
     return NAS_OK;
 }
 
+// all-gather each rank's per-pod lists (keys [np][KC] + bounds [np]) into
+// gk [world][np][KC] / gb [world][np] on `st` over communicator `cm`
+int exchange(nas_ctx *ctx, ncclComm *cm, hipStream_t st, const uint64_t *keys,
+             const uint64_t *bounds, size_t np, uint64_t *gk, uint64_t *gb) {
+    auto comm = reinterpret_cast<ncclComm_t>(cm);
+    ncclResult_t r = ncclGroupStart();
+    if (r == ncclSuccess) r = ncclAllGather(keys, gk, np * KC, ncclUint64, comm, st);
+    if (r == ncclSuccess) r = ncclAllGather(bounds, gb, np, ncclUint64, comm, st);
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess)
+        return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    return NAS_OK;
+}
+
+bool exchanging(const nas_ctx *ctx) { return ctx->world > 1 && !ctx->virtual_shard; }
+
 // scoring for pods [p_lo, p_hi) on stream st against capacity `cap`:
-// fit -> cost/top-k -> merge (-> exchange)
+// fit -> cost/top-k -> merge (-> exchange over the stream's communicator)
 int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nullptr,
                 const int32_t *cap = nullptr) {
     if (!st) st = ctx->stream;
     if (!cap) cap = ctx->cap.as<int32_t>();
+    const int sidx = st == ctx->stream2 ? 1 : 0;
     const int pr0 = p_lo / nas::COST_BN * nas::COST_BN;
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
     const int np = pr1 - pr0;
@@ -199,23 +224,16 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
                             (int64_t)ctx->Pp * KC, ctx->Pp, 0, p_lo, p_hi - p_lo,
                             ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>()));
-    if (ctx->world > 1 && !ctx->virtual_shard) {
+    if (exchanging(ctx)) {
         // exchange the per-shard lists of pods [pr0, pr1) and merge across ranks
-        auto comm = reinterpret_cast<ncclComm_t>(ctx->comm);
-        ncclResult_t r = ncclGroupStart();
-        if (r == ncclSuccess)
-            r = ncclAllGather(ctx->cand_key.as<uint64_t>() + (size_t)pr0 * KC,
-                              ctx->gather.as<uint64_t>(), (size_t)np * KC, ncclUint64, comm, st);
-        if (r == ncclSuccess)
-            r = ncclAllGather(ctx->cand_bound.as<uint64_t>() + pr0, ctx->gbound.as<uint64_t>(),
-                              (size_t)np, ncclUint64, comm, st);
-        ncclResult_t r2 = ncclGroupEnd();
-        if (r == ncclSuccess) r = r2;
-        if (r != ncclSuccess)
-            return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-        HIPCK(nas::launch_merge(st, ctx->gather.as<uint64_t>(), ctx->gbound.as<uint64_t>(),
-                                ctx->world, (int64_t)np * KC, np, pr0, p_lo, p_hi - p_lo,
-                                ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>()));
+        auto *gk = ctx->gather[sidx].as<uint64_t>();
+        auto *gb = ctx->gbound[sidx].as<uint64_t>();
+        OK(exchange(ctx, sidx ? ctx->comm2 : ctx->comm, st,
+                    ctx->cand_key.as<uint64_t>() + (size_t)pr0 * KC,
+                    ctx->cand_bound.as<uint64_t>() + pr0, (size_t)np, gk, gb));
+        HIPCK(nas::launch_merge(st, gk, gb, ctx->world, (int64_t)np * KC, np, pr0, p_lo,
+                                p_hi - p_lo, ctx->cand_key.as<uint64_t>(),
+                                ctx->cand_bound.as<uint64_t>()));
     }
     hipEvent_t e3 = tm.mark(st);
     tm.span(T_FIT, e0, e1);
@@ -223,6 +241,67 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     tm.span(T_MERGE, e2, e3);
     ctx->timings.cost_launches += 1;
     return NAS_OK;
+}
+
+// A rescore slot on the commit stream, enqueued behind a chunk's commit: if
+// the walk halted at pod s (halt word), rescore pods [s, min(s + RESCORE_PODS,
+// hi)) against the working capacity and resume the walk from s to hi; if it
+// did not halt, every kernel exits at once (the exchange still runs, so all
+// ranks issue the same collectives).  Every pod of [s, hi) belongs to chunks
+// whose scoring the commit stream has already waited for: no other stream
+// touches their masks, partial lists or candidate lists.
+int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi) {
+    int32_t *halt = ctx->status.as<int32_t>();
+    const nas::Dyn dyn{halt, RESCORE_PODS, hi};
+    auto *mask = ctx->mask.as<uint64_t>();
+    HIPCK(nas::launch_fit(sc, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
+                          ctx->req.as<int32_t>(), ctx->P, ctx->Pp, 0, RESCORE_PODS, mask, &dyn));
+    HIPCK(nas::launch_cost_topk(sc, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, ctx->Pp, 0,
+                                0, mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
+                                ctx->Nloc0, &dyn));
+    const int n_lists = ctx->Mp / nas::COST_BM;
+    if (!exchanging(ctx)) {
+        HIPCK(nas::launch_merge(sc, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
+                                n_lists, (int64_t)ctx->Pp * KC, ctx->Pp, 0, 0, 0,
+                                ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(), 0,
+                                &dyn, 0));
+    } else {
+        auto *rk = ctx->resc_key.as<uint64_t>();
+        auto *rb = ctx->resc_bound.as<uint64_t>();
+        auto *gk = ctx->gather_r.as<uint64_t>();
+        auto *gb = ctx->gbound_r.as<uint64_t>();
+        HIPCK(nas::launch_merge(sc, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
+                                n_lists, (int64_t)ctx->Pp * KC, ctx->Pp, 0, 0, 0, rk, rb, 0, &dyn,
+                                nas::MERGE_DST_WINDOW));
+        OK(exchange(ctx, ctx->comm_c, sc, rk, rb, RESCORE_PODS, gk, gb));
+        HIPCK(nas::launch_merge(sc, gk, gb, ctx->world, (int64_t)RESCORE_PODS * KC, RESCORE_PODS,
+                                0, 0, 0, ctx->cand_key.as<uint64_t>(),
+                                ctx->cand_bound.as<uint64_t>(), 0, &dyn, nas::MERGE_SRC_WINDOW));
+    }
+    HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                             ctx->req.as<int32_t>(), ctx->Pp, -1, hi, ctx->cap.as<int32_t>(),
+                             ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
+                             halt));
+    return NAS_OK;
+}
+
+// device-side rescore slots behind a chunk's commit (NAS_RESCORE_SLOTS
+// overrides the count for every chunk; read once)
+int rescore_slots(bool last) {
+    static const int n = [] {
+        const char *e = std::getenv("NAS_RESCORE_SLOTS");
+        return e ? std::max(0, std::atoi(e)) : -1;
+    }();
+    if (n >= 0) return n;
+    return last ? RESCORE_SLOTS_LAST : RESCORE_SLOTS;
+}
+
+// pods per pipelined scoring chunk: at least 32 pod tiles, and enough tiles
+// that one chunk's cost launch has ~640 workgroups on this rank's node tiles
+int chunk_pods(const nas_ctx *ctx) {
+    const int n_mt = ctx->Mp / nas::COST_BM;
+    const int tiles = std::max(32, (640 + n_mt - 1) / n_mt);
+    return tiles * nas::COST_BN;
 }
 
 int alloc_extended(nas_ctx *ctx) {
@@ -236,9 +315,15 @@ int alloc_extended(nas_ctx *ctx) {
     OK(nas::ensure(ctx, ctx->out_cost_i, (size_t)ctx->Pp * 4));
     OK(nas::ensure(ctx, ctx->status, 256));
     OK(nas::ensure(ctx, ctx->cap_snap, (size_t)3 * ctx->N * 4));
-    if (ctx->world > 1 && !ctx->virtual_shard) {
-        OK(nas::ensure(ctx, ctx->gather, (size_t)ctx->world * ctx->Pp * KC * 8));
-        OK(nas::ensure(ctx, ctx->gbound, (size_t)ctx->world * ctx->Pp * 8));
+    if (exchanging(ctx)) {
+        for (int i = 0; i < 2; ++i) {
+            OK(nas::ensure(ctx, ctx->gather[i], (size_t)ctx->world * ctx->Pp * KC * 8));
+            OK(nas::ensure(ctx, ctx->gbound[i], (size_t)ctx->world * ctx->Pp * 8));
+        }
+        OK(nas::ensure(ctx, ctx->resc_key, (size_t)RESCORE_PODS * KC * 8));
+        OK(nas::ensure(ctx, ctx->resc_bound, (size_t)RESCORE_PODS * 8));
+        OK(nas::ensure(ctx, ctx->gather_r, (size_t)ctx->world * RESCORE_PODS * KC * 8));
+        OK(nas::ensure(ctx, ctx->gbound_r, (size_t)ctx->world * RESCORE_PODS * 8));
     }
     if (!ctx->host_status.p) {
         HIPCK(hipHostMalloc(&ctx->host_status.p, 256, hipHostMallocDefault));
@@ -253,6 +338,13 @@ float decode_cost(uint32_t raw, int dtype) {
     float f;
     std::memcpy(&f, &u, 4);
     return f;
+}
+
+void destroy_comms(nas_ctx *ctx) {
+    for (ncclComm **c : {&ctx->comm, &ctx->comm2, &ctx->comm_c}) {
+        if (*c) (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(*c));
+        *c = nullptr;
+    }
 }
 
 }  // namespace
@@ -272,10 +364,15 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
     nas_ctx *ctx = new (std::nothrow) nas_ctx();
     if (!ctx) return NAS_ERR_NOMEM;
     ctx->device = dev;
+    // the commit stream runs at the highest priority: its one-workgroup walks
+    // and rescore slots take the next CU a scoring workgroup frees instead of
+    // queueing behind a whole scoring launch
+    int prio_lo = 0, prio_hi = 0;
     if (hipSetDevice(dev) != hipSuccess ||
+        hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->stream_commit, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithPriority(&ctx->stream_commit, hipStreamNonBlocking, prio_hi) != hipSuccess) {
         delete ctx;
         return NAS_ERR_HIP;
     }
@@ -292,12 +389,14 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->pod_snap, &ctx->best, &ctx->winners, &ctx->snap_best, &ctx->snap_win,
                       &ctx->Lt, &ctx->WA, &ctx->cap0, &ctx->cap, &ctx->cap_snap, &ctx->req, &ctx->mask,
                       &ctx->partial, &ctx->pbound, &ctx->cand_key, &ctx->cand_bound,
-                      &ctx->gather, &ctx->gbound, &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
+                      &ctx->gather[0], &ctx->gbound[0], &ctx->gather[1], &ctx->gbound[1],
+                      &ctx->resc_key, &ctx->resc_bound, &ctx->gather_r, &ctx->gbound_r,
+                      &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
                       &ctx->status, &ctx->scratch};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
-    if (ctx->comm) (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(ctx->comm));
+    destroy_comms(ctx);
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->stream2);
     (void)hipStreamDestroy(ctx->stream_commit);
@@ -605,31 +704,43 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     const int P = ctx->P, N = ctx->N;
     int32_t *halt = ctx->status.as<int32_t>();
     hipEvent_t t0 = tm.mark(st);
-    // the scoring pass filters against the capacity at entry, while the
-    // commit walks (stream_commit) consume the working capacity behind it
-    HIPCK(hipMemcpyAsync(ctx->cap_snap.p, ctx->cap.p, (size_t)3 * N * 4, hipMemcpyDeviceToDevice, st));
-    HIPCK(hipMemsetAsync(halt, 0xff, 16, st));  // halt = -1
+    // Each chunk is filtered against the working capacity as the commit
+    // stream has left it so far: every value read is >= the capacity at the
+    // chunk's pods' own (later) turn, so every node that will fit them is
+    // scored (the lists stay exact) and the lists are far fresher than a
+    // snapshot at entry -- fewer pods exhaust them.  Only the LDS commit
+    // publishes final values alone; the L2 commit's speculative reservations
+    // could dip below them, so it scores against a snapshot at entry.
+    const bool live_cap = nas::commit_in_lds(N);
+    const int32_t *score_cap = live_cap ? ctx->cap.as<int32_t>() : ctx->cap_snap.as<int32_t>();
+    if (!live_cap)
+        HIPCK(hipMemcpyAsync(ctx->cap_snap.p, ctx->cap.p, (size_t)3 * N * 4, hipMemcpyDeviceToDevice, st));
+    HIPCK(hipMemsetAsync(halt, 0xff, 4, st));  // halt = -1
+    HIPCK(hipMemsetAsync(halt + 1, 0, 4, st));  // device-side rescore count
     hipEvent_t ready = tm.mark(st);
     HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
     HIPCK(hipStreamWaitEvent(sc, ready, 0));
-    for (int c = 0, lo = 0; lo < P; ++c, lo += CHUNK_PODS) {
-        const int hi = std::min(P, lo + CHUNK_PODS);
-        // two scoring streams: a chunk's tail blocks overlap the next chunk
-        // (multi-GPU keeps one stream so every rank issues its collectives in order)
-        hipStream_t ss = (ctx->world == 1 && (c & 1)) ? ctx->stream2 : st;
-        OK(score_range(ctx, tm, lo, hi, ss, ctx->cap_snap.as<int32_t>()));
+    const int cp = chunk_pods(ctx);
+    for (int c = 0, lo = 0; lo < P; ++c, lo += cp) {
+        const int hi = std::min(P, lo + cp);
+        // two scoring streams (each with its own communicator when sharded):
+        // a chunk's tail blocks overlap the next chunk
+        hipStream_t ss = (c & 1) ? ctx->stream2 : st;
+        OK(score_range(ctx, tm, lo, hi, ss, score_cap));
         HIPCK(hipStreamWaitEvent(sc, tm.mark(ss), 0));
         hipEvent_t c0 = tm.mark(sc);
         HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt));
+        for (int r = 0, n = rescore_slots(hi == P); r < n; ++r) OK(rescore_slot(ctx, sc, hi));
         tm.span(T_COMMIT, c0, tm.mark(sc));
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
     HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
     int32_t *hs = ctx->host_status.as<int32_t>();
-    HIPCK(hipMemcpyAsync(hs, halt, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hs, halt, 8, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    const int dev_rounds = hs[1];
     int rounds = 0;
     while (hs[0] >= 0) {
         // pod `stop` exhausted its candidates: rescore a window against the
@@ -639,7 +750,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         if (stop >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
         if (++rounds > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
         OK(score_range(ctx, tm, stop, std::min(P, stop + RESCORE_PODS)));
-        HIPCK(hipMemsetAsync(halt, 0xff, 16, st));
+        HIPCK(hipMemsetAsync(halt, 0xff, 4, st));
         hipEvent_t c0 = tm.mark(st);
         HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, stop, P, ctx->cap.as<int32_t>(), N,
@@ -671,7 +782,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     ctx->timings.merge_ms = tm.total(T_MERGE);
     ctx->timings.commit_ms = tm.total(T_COMMIT);
     ctx->timings.total_ms = tm.total(T_TOTAL);
-    ctx->timings.rescore_rounds = rounds;
+    ctx->timings.rescore_rounds = rounds + dev_rounds;
     ctx->timings.unschedulable = unsched;
     ctx->scored = true;
     return NAS_OK;
@@ -723,21 +834,28 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
         return nas::fail(ctx, NAS_ERR_ARG, "nas_comm_init: rank/world");
     if (ctx->have_L || ctx->have_wa || ctx->have_cap)
         return nas::fail(ctx, NAS_ERR_STATE, "nas_comm_init must precede the extended uploads");
-    if (ctx->comm) {
-        (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(ctx->comm));
-        ctx->comm = nullptr;
-    }
+    destroy_comms(ctx);
     ctx->rank = rank;
     ctx->world = world;
     ctx->virtual_shard = false;
     if (world == 1) return NAS_OK;
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
-    ncclComm_t comm;
+    ncclComm_t comm, comm2 = nullptr, comm_c = nullptr;
     ncclResult_t r = ncclCommInitRank(&comm, world, uid, rank);
     if (r != ncclSuccess)
         return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     ctx->comm = reinterpret_cast<ncclComm *>(comm);
+    // one communicator per stream that issues collectives (second scoring
+    // stream, commit stream): each keeps its own issue order on every rank
+    r = ncclCommSplit(comm, 0, rank, &comm2, nullptr);
+    if (r == ncclSuccess) r = ncclCommSplit(comm, 0, rank, &comm_c, nullptr);
+    ctx->comm2 = reinterpret_cast<ncclComm *>(comm2);
+    ctx->comm_c = reinterpret_cast<ncclComm *>(comm_c);
+    if (r != ncclSuccess) {
+        destroy_comms(ctx);
+        return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclCommSplit: ") + ncclGetErrorString(r));
+    }
     return NAS_OK;
 }
 

@@ -70,15 +70,17 @@ struct nas_ctx {
     nas::DevBuf Lt;          // [Mp][Kp] elements: Lt[i][m] = L[m][Nloc0 + i]
     nas::DevBuf WA;          // [Pp][Kp] elements
     nas::DevBuf cap0, cap;   // [3][N] int32 (initial, working)
-    nas::DevBuf cap_snap;    // [3][N] working capacity at the start of nas_place
+    nas::DevBuf cap_snap;    // [3][N] working capacity at the start of nas_place (L2 commit)
     nas::DevBuf req;         // [3][Pp] int32
     nas::DevBuf mask;        // [ceil(Mp/64)][Pp] uint64, local nodes
     nas::DevBuf partial;     // [Mp/BM][Pp][KC] uint64 keys per node tile
     nas::DevBuf pbound;      // [Mp/BM][Pp] uint64 exactness bound per node tile
     nas::DevBuf cand_key;    // [Pp][KC] uint64 (global node ids), after merge
     nas::DevBuf cand_bound;  // [Pp] uint64
-    nas::DevBuf gather;      // [world][Pp][KC] uint64 (multi-GPU exchange)
-    nas::DevBuf gbound;      // [world][Pp] uint64
+    nas::DevBuf gather[2];   // per scoring stream: [world][chunk][KC] uint64 (multi-GPU exchange)
+    nas::DevBuf gbound[2];   // per scoring stream: [world][chunk] uint64
+    nas::DevBuf resc_key, resc_bound;      // rescore slot staging [win][KC] / [win] (multi-GPU)
+    nas::DevBuf gather_r, gbound_r;        // rescore slot exchange [world][win][KC] / [world][win]
     nas::DevBuf out_node, out_cost_f, out_cost_i;  // [Pp]
     nas::DevBuf status;      // small device scratch for commit control
     nas::DevBuf host_status; // pinned
@@ -88,7 +90,9 @@ struct nas_ctx {
     uint64_t synth_seed = 0;
 
     // ---- multi-GPU
-    ncclComm *comm = nullptr;
+    ncclComm *comm = nullptr;    // scoring chunks on `stream` and host-side rescores
+    ncclComm *comm2 = nullptr;   // scoring chunks on `stream2`
+    ncclComm *comm_c = nullptr;  // rescore slots on `stream_commit`
     int32_t rank = 0, world = 1;
     bool virtual_shard = false;  // nas_set_shard: shard geometry, no exchange
 };
@@ -105,15 +109,32 @@ hipError_t launch_vote_gather(hipStream_t st, const int32_t *pod_snap, int P,
                               const int32_t *snap_best, const int32_t *snap_win, int32_t *best,
                               int32_t *win);
 
+// A rescore slot's pod window, decided on the device: the kernels read the
+// window start from *start (the commit's halt word; < 0 = nothing to do) and
+// cover pods [start, min(start + win, hi)).  Grids are sized for `win`.
+struct Dyn {
+    const int32_t *start;
+    int win;
+    int hi;
+};
+constexpr int MERGE_SRC_WINDOW = 1;  // k_merge source lists indexed from the window start
+constexpr int MERGE_DST_WINDOW = 2;  // k_merge destination indexed from the window start
+
 hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nloc, int Mp,
-                      const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask);
+                      const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask,
+                      const Dyn *dyn = nullptr);
 
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
-                            uint64_t *partial, uint64_t *pbound, int node_base);
+                            uint64_t *partial, uint64_t *pbound, int node_base,
+                            const Dyn *dyn = nullptr);
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
-                        uint64_t *cand_key, uint64_t *cand_bound);
+                        uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,
+                        const Dyn *dyn = nullptr, int dyn_flags = 0);
+// the commit keeps the working capacity in LDS (and publishes only final
+// values, at the end of each launch) for clusters of up to this many nodes
+bool commit_in_lds(int N);
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost_i, int32_t *halt);

@@ -49,11 +49,12 @@ int main(int argc, char **argv) {
     const u64 *mk = (const u64 *)mask;
     u64 *pa = (u64 *)partial, *pb = (u64 *)pbound;
     int zero = 0;
+    const int *nodyn = nullptr;
     for (int r = 0; r < reps; ++r) {
         for (int v = 0; v < nv; ++v) {
             if (!strchr(vsel, 'a' + v)) continue;
             void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero,
-                            (void *)&Pp, &mk, &pa, &pb, &zero};
+                            (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero};
             CK(hipEventRecord(a));
             CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(THREADS), args, vars[v].lds, 0));
             CK(hipEventRecord(b));

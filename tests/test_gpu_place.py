@@ -245,3 +245,19 @@ def test_commit_huge_requests_no_overflow(engine):
     assert ci.tolist() == wcost.tolist()
     assert (engine.get_capacity() == wfree).all()
     assert (want < 0).sum() > 0  # the cluster overflows: unschedulable pods exist
+
+
+def test_rescore_slots_across_chunks(engine):
+    """Many commit stops spread over several 8192-pod scoring chunks: the
+    device-side rescore slots behind each chunk's commit, and the host loop
+    for stops beyond them, reproduce the sequential oracle exactly."""
+    rng = np.random.default_rng(21)
+    P, N = 20000, 256
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=30, cap_scale=0.6)
+    WA[:, :24] = 127  # everyone prefers nodes 0..23, which fill up early
+    upload(engine, WA, L, free, req, "i8")
+    node, _, ci = engine.place()
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    assert engine.timings()["rescore_rounds"] > 3
+    assert node.tolist() == want.tolist() and ci.tolist() == wcost.tolist()
+    assert (engine.get_capacity() == wfree).all()
