@@ -29,6 +29,8 @@
 // partial[node_tile][pod][8] + pbound[node_tile][pod] (72 B per pod per tile).
 #include "klist.h"
 
+#include <type_traits>
+
 namespace nas {
 namespace {
 
@@ -52,8 +54,10 @@ constexpr int TILE_BYTES = BM * BKB;          // 32 KiB: one operand, one stage
 // PIPE 0: A and B double-buffered (128 KiB).  PIPE 1: A (latency rows, mostly
 // L2/MALL-resident) double-buffered, B (the 1 GB traffic stream, mostly HBM)
 // triple-buffered so its loads get two K-steps of cover (160 KiB, all of LDS).
+// PIPE 2: as 0, but B is staged through registers (global_load_dwordx4 ->
+// ds_write_b128) instead of LDS-DMA; PIPE 3: both operands register-staged.
 template <int PIPE>
-constexpr int lds_bytes() { return PIPE == 0 ? 2 * STAGE_BYTES : 5 * TILE_BYTES; }
+constexpr int lds_bytes() { return PIPE == 1 ? 5 * TILE_BYTES : 2 * STAGE_BYTES; }
 #ifndef COST_SCHED
 #define COST_SCHED 1
 #endif
@@ -165,10 +169,10 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // buffer b of operand A / B (PIPE 0: A|B interleaved per stage; PIPE 1:
     // A0 A1 B0 B1 B2)
     auto abuf = [&](int b) -> unsigned char * {
-        return PIPE == 0 ? lds + b * STAGE_BYTES : lds + b * TILE_BYTES;
+        return PIPE != 1 ? lds + b * STAGE_BYTES : lds + b * TILE_BYTES;
     };
     auto bbuf = [&](int b) -> unsigned char * {
-        return PIPE == 0 ? lds + b * STAGE_BYTES + TILE_BYTES : lds + (2 + b) * TILE_BYTES;
+        return PIPE != 1 ? lds + b * STAGE_BYTES + TILE_BYTES : lds + (2 + b) * TILE_BYTES;
     };
     // one 1 KiB LDS-DMA piece (8 rows x 128 B) of operand A / B: piece j of
     // wave w fills rows (8j + w)*8 .. +8
@@ -286,6 +290,138 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
             }
+        }
+    } else if constexpr (PIPE == 4) {
+        // Phased, staggered pipeline.  Each K-step is 4 phases (one 32-byte
+        // k-substep each); a phase is a LOAD segment (the next phase's 6
+        // fragment ds_reads + this wave's share of the next stage's LDS-DMA)
+        // and an MFMA segment (8 MFMAs at s_setprio 1), each closed by a raw
+        // s_barrier.  Waves 4-7 run one barrier behind waves 0-3, so on every
+        // SIMD one wave's MFMA segment overlaps its partner's load segment.
+        // Stage t+1 is issued in phases 0-1 of step t (4 pieces each), retired
+        // by a vmcnt(0) in phase 2's load segment and first read in phase 3's
+        // (a barrier apart, for both wave groups); its buffer's previous
+        // reads ended in phase 2 of step t-1.  No __syncthreads in the loop:
+        // its fence would drain the DMA.
+        v4i fa[2][4], fb[2][2];
+        auto readf = [&](int buf, int kk, v4i (&ra)[4], v4i (&rb)[2]) {
+            const unsigned char *As = abuf(buf);
+            const unsigned char *Bs = bbuf(buf);
+            const int c = kk * 2 + fh;
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int r = wm * 128 + mi * 32 + fr;
+                ra[mi] = *reinterpret_cast<const v4i *>(As + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int r = wn * 64 + ni * 32 + fr;
+                rb[ni] = *reinterpret_cast<const v4i *>(Bs + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+        };
+        auto mma8 = [&](const v4i (&ra)[4], const v4i (&rb)[2]) {
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = M::mma(ra[mi], rb[ni], acc[mi][ni]);
+            __builtin_amdgcn_s_setprio(0);
+        };
+        auto bar = [] {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // prologue: stage 0, fragments of (0, 0), then the stagger
+        stageA(0, 0);
+        stageB(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        readf(0, 0, fa[0], fb[0]);
+        if (wm == 1) bar();
+        // one K-step; MORE = a next stage exists (the last step is peeled, so
+        // the steady-state body is one basic block: hipcc's waitcnt pass then
+        // keeps the next phase's ds_reads in flight over the MFMA segment)
+        auto step = [&](int t, auto more_c) {
+            constexpr bool MORE = decltype(more_c)::value;
+            const int cur = t & 1;
+            const int kn = (t + 1) * BKB;
+            // phase 0 (fragment reads first, then the DMA pieces)
+            readf(cur, 1, fa[1], fb[1]);
+            if constexpr (MORE) {
+                pieceA(cur ^ 1, kn, 0); pieceA(cur ^ 1, kn, 1);
+                pieceB(cur ^ 1, kn, 0); pieceB(cur ^ 1, kn, 1);
+            }
+            bar();
+            mma8(fa[0], fb[0]);
+            bar();
+            // phase 1
+            readf(cur, 2, fa[0], fb[0]);
+            if constexpr (MORE) {
+                pieceA(cur ^ 1, kn, 2); pieceA(cur ^ 1, kn, 3);
+                pieceB(cur ^ 1, kn, 2); pieceB(cur ^ 1, kn, 3);
+            }
+            bar();
+            mma8(fa[1], fb[1]);
+            bar();
+            // phase 2: retire this wave's pieces of stage t+1 (vmcnt(0) only)
+            if constexpr (MORE) __builtin_amdgcn_s_waitcnt(0x0F70);
+            readf(cur, 3, fa[1], fb[1]);
+            bar();
+            mma8(fa[0], fb[0]);
+            bar();
+            // phase 3
+            if constexpr (MORE) readf(cur ^ 1, 0, fa[0], fb[0]);
+            bar();
+            mma8(fa[1], fb[1]);
+            bar();
+        };
+        for (int t = 0; t + 1 < nk; ++t) step(t, std::true_type{});
+        step(nk - 1, std::false_type{});
+        if (wm == 0) bar();  // re-align the barrier count of the two groups
+        __syncthreads();
+    } else if constexpr (PIPE >= 2) {
+        // register-staged operands: step t+1's rows are loaded into VGPRs at
+        // the top of step t (latency hidden by its MFMAs) and written to the
+        // other LDS buffer (same swizzled image as the DMA path) at its end
+        v4i rb[4], ra[4];
+        auto gload = [&](const unsigned char *G, int k0, v4i (&r)[4]) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = (j * 8 + w) * 8 + srow_in;
+                r[j] = *reinterpret_cast<const v4i *>(G + (size_t)row * Kb + k0 + sq * 16);
+            }
+        };
+        auto lwrite = [&](unsigned char *L, const v4i (&r)[4]) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = (j * 8 + w) * 8 + srow_in;
+                const int c = sq ^ ((row >> 1) & 7);
+                *reinterpret_cast<v4i *>(L + row * BKB + c * 16) = r[j];
+            }
+        };
+        if constexpr (PIPE == 2) stageA(0, 0);
+        else gload(Ag, 0, ra);
+        gload(Bg, 0, rb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (PIPE == 3) lwrite(abuf(0), ra);
+        lwrite(bbuf(0), rb);
+        __syncthreads();
+        for (int t = 0; t < nk; ++t) {
+            const int cur = t & 1;
+            const bool more = t + 1 < nk;
+            if (more) {
+                if constexpr (PIPE == 2) stageA(cur ^ 1, (t + 1) * BKB);
+                else gload(Ag, (t + 1) * BKB, ra);
+                gload(Bg, (t + 1) * BKB, rb);
+            }
+            compute(cur, cur, nopiece);
+            if (more) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if constexpr (PIPE == 3) lwrite(abuf(cur ^ 1), ra);
+                lwrite(bbuf(cur ^ 1), rb);
+            }
+            __syncthreads();
         }
     } else if constexpr (PIPE == 0) {
         // two-stage pipeline: stage t+1 streams in (LDS-DMA) while t is read
@@ -484,6 +620,9 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
         u64 *, int, const int *, int);
 NAS_INST(0, 0, 0, 4) NAS_INST(1, 0, 0, 4) NAS_INST(0, 5, 0, 4) NAS_INST(1, 5, 0, 4)
 NAS_INST(3, 5, 0, 4) NAS_INST(0, 1, 0, 4) NAS_INST(0, 5, 0, 8) NAS_INST(4, 0, 0, 4)
+NAS_INST(0, 1, 2, 4) NAS_INST(0, 1, 3, 4) NAS_INST(0, 0, 2, 4) NAS_INST(0, 0, 3, 4)
+NAS_INST(1, 1, 2, 4) NAS_INST(1, 1, 3, 4)
+NAS_INST(0, 0, 4, 4) NAS_INST(1, 0, 4, 4) NAS_INST(0, 0, 4, 8) NAS_INST(0, 0, 4, 2)
 #undef NAS_INST
 #endif
 

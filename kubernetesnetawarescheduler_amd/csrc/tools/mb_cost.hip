@@ -36,7 +36,12 @@ int main(int argc, char **argv) {
     const V vars[] = {{"top4/jit", KV(0, 0, 0, 4)},   {"noepi/jit", KV(1, 0, 0, 4)},
                       {"top4/spread", KV(0, 5, 0, 4)}, {"noepi/spread", KV(1, 5, 0, 4)},
                       {"l2hot/spread", KV(3, 5, 0, 4)}, {"top4/pin", KV(0, 1, 0, 4)},
-                      {"top4/spr/g8", KV(0, 5, 0, 8)}, {"ldsonly+bar", KV(4, 0, 0, 4)}};
+                      {"top4/spr/g8", KV(0, 5, 0, 8)}, {"ldsonly+bar", KV(4, 0, 0, 4)},
+                      {"top4/pin/regB", KV(0, 1, 2, 4)}, {"top4/pin/regAB", KV(0, 1, 3, 4)},
+                      {"top4/jit/regB", KV(0, 0, 2, 4)}, {"top4/jit/regAB", KV(0, 0, 3, 4)},
+                      {"noepi/pin/regB", KV(1, 1, 2, 4)}, {"noepi/pin/regAB", KV(1, 1, 3, 4)},
+                      {"top4/phased", KV(0, 0, 4, 4)}, {"noepi/phased", KV(1, 0, 4, 4)},
+                      {"top4/phased/g8", KV(0, 0, 4, 8)}, {"top4/phased/g2", KV(0, 0, 4, 2)}};
     const int nv = sizeof(vars) / sizeof(vars[0]);
     for (int v = 0; v < nv; ++v)
         CK(hipFuncSetAttribute(vars[v].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[v].lds));
