@@ -88,7 +88,7 @@ typedef struct nas_timings {
     int32_t cost_launches;   /* launches of the contraction kernel */
     int32_t rescore_rounds;  /* commit stops that needed a rescore */
     int32_t unschedulable;   /* pods with no fitting node */
-    int32_t reserved;
+    int32_t commit_rounds;   /* rounds of the parallel commit walk (all windows) */
 } nas_timings;
 
 /* ---- lifecycle --------------------------------------------------------- */
@@ -208,6 +208,42 @@ int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world);
  * << 32 | global node index, ascending; ~0 = empty) and bounds[P] (every
  * fitting key <= bound is in the list; ~0 = nothing was dropped). */
 int nas_get_candidate_keys(nas_ctx *ctx, uint64_t *keys, uint64_t *bounds);
+
+/* ---- host-driven steps of nas_place -------------------------------------
+ * For hosts that run the placement loop themselves -- e.g. node shards
+ * (nas_set_shard) whose candidate lists travel over the host's own
+ * transport: score a pod range on this context's node columns, read the raw
+ * lists, write back the lists merged across shards, and commit:
+ *
+ *   nas_score_range(0, P) -> get keys -> [exchange + merge] -> set keys
+ *   stop = 0; while (stop < P) {
+ *     nas_commit(stop, ..., &stop);          // replicated on every shard
+ *     if (stop < P) { nas_score_range(stop, min(P, stop + 1024)); get/merge/set }
+ *   }
+ *
+ * Merge rule for lists of several shards: keep the 8 smallest keys, bound =
+ * min(all bounds, kept[7]).  Every shard runs the same commit on the same
+ * merged lists, so all of them return the same placements. */
+
+/* Scoring pass (fit against the WORKING capacity, cost/top-k, merge over
+ * this context's node tiles) for pods [p_lo, p_hi). */
+int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi);
+
+/* Raw candidate lists of pods [p_lo, p_lo + n): keys[n*8], bounds[n]
+ * (encoding of nas_get_candidate_keys). */
+int nas_get_candidate_keys_range(nas_ctx *ctx, int32_t p_lo, int32_t n, uint64_t *keys,
+                                 uint64_t *bounds);
+int nas_set_candidate_keys(nas_ctx *ctx, int32_t p_lo, int32_t n, const uint64_t *keys,
+                           const uint64_t *bounds);
+
+/* Greedy commit of pods [p_begin, P) in order on the current lists and the
+ * working capacity.  Stops at the first pod none of whose usable candidates
+ * fits while its list is incomplete (score it again first): *stop_out = that
+ * pod, or P when every pod was placed.  node_out / cost_out / int_score_out
+ * (length P; cost_out and int_score_out may be NULL) receive entries
+ * [p_begin, *stop_out) only. */
+int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out,
+               int64_t *int_score_out, int32_t *stop_out);
 
 /* ---- synthetic inputs generated in HBM (benchmarks; seeded, deterministic) */
 /* Reference-mode snapshots per SURVEY.md §8(d) C1/C3. */

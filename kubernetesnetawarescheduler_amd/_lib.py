@@ -47,10 +47,10 @@ class NasTimings(ctypes.Structure):
                 ("merge_ms", ctypes.c_float), ("commit_ms", ctypes.c_float),
                 ("vote_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
                 ("cost_launches", ctypes.c_int32), ("rescore_rounds", ctypes.c_int32),
-                ("unschedulable", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("unschedulable", ctypes.c_int32), ("commit_rounds", ctypes.c_int32)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _c = ctypes
@@ -83,6 +83,10 @@ SIGNATURES = {
     "nas_comm_init": (_I, [_CTX, _V, _I, _I]),
     "nas_set_shard": (_I, [_CTX, _I, _I]),
     "nas_get_candidate_keys": (_I, [_CTX, _V, _V]),
+    "nas_score_range": (_I, [_CTX, _I, _I]),
+    "nas_get_candidate_keys_range": (_I, [_CTX, _I, _I, _V, _V]),
+    "nas_set_candidate_keys": (_I, [_CTX, _I, _I, _V, _V]),
+    "nas_commit": (_I, [_CTX, _I, _V, _V, _V, _V]),
     "nas_synth_snapshots": (_I, [_CTX, _c.c_uint64, _I, _I]),
     "nas_read_snapshot": (_I, [_CTX, _I, _V, _V, _V, _V, _V, _V]),
     "nas_synth_cluster": (_I, [_CTX, _c.c_uint64, _I, _I, _I, _I]),

@@ -129,21 +129,22 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             // first barrier and is next written after this round's: reset it
             if (tid == 0) first_bad[(round + 1) % 3] = NO_POD;
             // 1. pick against the capacity at the start of the round, reserve
-            bool fit[KC];
-#pragma unroll
-            for (int j = 0; j < KC; ++j) {
-                const bool usable = cur.k[j] != KEY_INVALID && cur.k[j] <= cur.bound;
-                const int n = usable ? (int)(unsigned)cur.k[j] : 0;
-                const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
-                fit[j] = usable && cur.r0 <= a && cur.r1 <= b && cur.r2 <= c;
-            }
+            // candidates in list order, stopping at the first that fits (most
+            // pods stop at their first): 3 LDS reads per candidate looked at
             int choice = -1;
             unsigned ccost = 0;
+            if (!done) {
 #pragma unroll
-            for (int j = KC - 1; j >= 0; --j) {
-                if (fit[j]) {
-                    choice = (int)(unsigned)cur.k[j];
-                    ccost = (unsigned)(cur.k[j] >> 32);
+                for (int j = 0; j < KC; ++j) {
+                    const u64 k = cur.k[j];
+                    if (k == KEY_INVALID || k > cur.bound) break;  // end of the usable prefix
+                    const int n = (int)(unsigned)k;
+                    const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
+                    if (cur.r0 <= a && cur.r1 <= b && cur.r2 <= c) {
+                        choice = n;
+                        ccost = (unsigned)(k >> 32);
+                        break;
+                    }
                 }
             }
             if (done) choice = -1;
@@ -213,7 +214,10 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         if (stop < p_end) break;
         if (base + THREADS < p_end) cur = nxt;
     }
-    if (tid == 0 && stop < p_end) *halt = stop;
+    if (tid == 0) {
+        if (stop < p_end) *halt = stop;
+        halt[2] += round;  // rounds walked, reported in nas_timings
+    }
     __syncthreads();
     if (LDS_CAP)
         for (int i = tid; i < 3 * N; i += THREADS) cap_g[i] = capl[i];

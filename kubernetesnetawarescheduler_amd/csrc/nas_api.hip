@@ -297,10 +297,12 @@ int rescore_slots(bool last) {
 }
 
 // pods per pipelined scoring chunk: at least 32 pod tiles, and enough tiles
-// that one chunk's cost launch has ~640 workgroups on this rank's node tiles
-int chunk_pods(const nas_ctx *ctx) {
+// that one chunk's cost launch has ~512 workgroups on this rank's node tiles
+// (node shards have few node tiles).  The first chunk is always 32 tiles, so
+// the commit stream starts early.
+int chunk_pods(const nas_ctx *ctx, int c) {
     const int n_mt = ctx->Mp / nas::COST_BM;
-    const int tiles = std::max(32, (640 + n_mt - 1) / n_mt);
+    const int tiles = c == 0 ? 32 : std::max(32, (512 + n_mt - 1) / n_mt);
     return tiles * nas::COST_BN;
 }
 
@@ -716,13 +718,12 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     if (!live_cap)
         HIPCK(hipMemcpyAsync(ctx->cap_snap.p, ctx->cap.p, (size_t)3 * N * 4, hipMemcpyDeviceToDevice, st));
     HIPCK(hipMemsetAsync(halt, 0xff, 4, st));  // halt = -1
-    HIPCK(hipMemsetAsync(halt + 1, 0, 4, st));  // device-side rescore count
+    HIPCK(hipMemsetAsync(halt + 1, 0, 8, st));  // device-side rescores, commit rounds
     hipEvent_t ready = tm.mark(st);
     HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
     HIPCK(hipStreamWaitEvent(sc, ready, 0));
-    const int cp = chunk_pods(ctx);
-    for (int c = 0, lo = 0; lo < P; ++c, lo += cp) {
-        const int hi = std::min(P, lo + cp);
+    for (int c = 0, lo = 0, hi = 0; lo < P; ++c, lo = hi) {
+        hi = std::min(P, lo + chunk_pods(ctx, c));
         // two scoring streams (each with its own communicator when sharded):
         // a chunk's tail blocks overlap the next chunk
         hipStream_t ss = (c & 1) ? ctx->stream2 : st;
@@ -738,7 +739,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
     HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
     int32_t *hs = ctx->host_status.as<int32_t>();
-    HIPCK(hipMemcpyAsync(hs, halt, 8, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hs, halt, 12, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     const int dev_rounds = hs[1];
     int rounds = 0;
@@ -759,6 +760,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         HIPCK(hipMemcpyAsync(hs, halt, 4, hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
     }
+    HIPCK(hipMemcpyAsync(hs + 2, halt + 2, 4, hipMemcpyDeviceToHost, st));
     std::vector<uint32_t> raw;
     HIPCK(hipMemcpyAsync(node_out, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
     if (cost_out || int_score_out) {
@@ -784,6 +786,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     ctx->timings.total_ms = tm.total(T_TOTAL);
     ctx->timings.rescore_rounds = rounds + dev_rounds;
     ctx->timings.unschedulable = unsched;
+    ctx->timings.commit_rounds = hs[2];
     ctx->scored = true;
     return NAS_OK;
 }
@@ -815,6 +818,118 @@ int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i, f
         if (count) count[p] = c;
         if (complete) complete[p] = bounds[p] == nas::KEY_INVALID;
     }
+    return NAS_OK;
+}
+
+// ------------------------------------------------------- host-driven steps
+int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi) {
+    OK(bind(ctx));
+    OK(check_extended(ctx));
+    if (p_lo < 0 || p_hi > ctx->P || p_lo >= p_hi)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_score_range: pod range");
+    OK(alloc_extended(ctx));
+    std::memset(&ctx->timings, 0, sizeof(ctx->timings));
+    Timer tm(ctx);
+    OK(score_range(ctx, tm, p_lo, p_hi));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->timings.fit_ms = tm.total(T_FIT);
+    ctx->timings.cost_ms = tm.total(T_COST);
+    ctx->timings.merge_ms = tm.total(T_MERGE);
+    ctx->scored = true;
+    return NAS_OK;
+}
+
+static int keys_range_ok(nas_ctx *ctx, int32_t p_lo, int32_t n, const void *keys,
+                         const void *bounds) {
+    if (!ctx->cand_key.p) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
+    if (p_lo < 0 || n < 0 || p_lo + n > ctx->P || (n > 0 && (!keys || !bounds)))
+        return nas::fail(ctx, NAS_ERR_ARG, "candidate key range");
+    return NAS_OK;
+}
+
+int nas_get_candidate_keys_range(nas_ctx *ctx, int32_t p_lo, int32_t n, uint64_t *keys,
+                                 uint64_t *bounds) {
+    OK(bind(ctx));
+    OK(keys_range_ok(ctx, p_lo, n, keys, bounds));
+    if (n == 0) return NAS_OK;
+    HIPCK(hipMemcpyAsync(keys, ctx->cand_key.as<uint64_t>() + (size_t)p_lo * KC, (size_t)n * KC * 8,
+                         hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipMemcpyAsync(bounds, ctx->cand_bound.as<uint64_t>() + p_lo, (size_t)n * 8,
+                         hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    return NAS_OK;
+}
+
+int nas_set_candidate_keys(nas_ctx *ctx, int32_t p_lo, int32_t n, const uint64_t *keys,
+                           const uint64_t *bounds) {
+    OK(bind(ctx));
+    OK(keys_range_ok(ctx, p_lo, n, keys, bounds));
+    // the commit relies on sorted lists with in-range node ids
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        const uint64_t *k = keys + i * KC;
+        for (int j = 0; j < KC; ++j) {
+            if (j && k[j] < k[j - 1])
+                return nas::fail(ctx, NAS_ERR_ARG, "candidate keys not ascending");
+            if (k[j] != nas::KEY_INVALID && (int64_t)(uint32_t)k[j] >= ctx->N)
+                return nas::fail(ctx, NAS_ERR_ARG, "candidate key names a node out of range");
+        }
+    }
+    if (n == 0) return NAS_OK;
+    HIPCK(hipMemcpyAsync(ctx->cand_key.as<uint64_t>() + (size_t)p_lo * KC, keys, (size_t)n * KC * 8,
+                         hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->cand_bound.as<uint64_t>() + p_lo, bounds, (size_t)n * 8,
+                         hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->scored = true;
+    return NAS_OK;
+}
+
+int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out,
+               int64_t *int_score_out, int32_t *stop_out) {
+    OK(bind(ctx));
+    OK(check_extended(ctx));
+    if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "nas_commit needs candidate lists");
+    if (!node_out || !stop_out || p_begin < 0 || p_begin > ctx->P)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_commit arguments");
+    const int P = ctx->P;
+    *stop_out = P;
+    if (p_begin == P) return NAS_OK;
+    std::memset(&ctx->timings, 0, sizeof(ctx->timings));
+    Timer tm(ctx);
+    hipStream_t st = ctx->stream;
+    int32_t *halt = ctx->status.as<int32_t>();
+    HIPCK(hipMemsetAsync(halt, 0xff, 4, st));
+    HIPCK(hipMemsetAsync(halt + 1, 0, 8, st));
+    hipEvent_t c0 = tm.mark(st);
+    HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                             ctx->req.as<int32_t>(), ctx->Pp, p_begin, P, ctx->cap.as<int32_t>(),
+                             ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
+                             halt));
+    tm.span(T_COMMIT, c0, tm.mark(st));
+    int32_t *hs = ctx->host_status.as<int32_t>();
+    HIPCK(hipMemcpyAsync(hs, halt, 12, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    const int stop = hs[0] >= 0 ? hs[0] : P;
+    if (stop < p_begin || stop > P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
+    const int n = stop - p_begin;
+    std::vector<uint32_t> raw(n);
+    if (n) {
+        HIPCK(hipMemcpyAsync(node_out + p_begin, ctx->out_node.as<int32_t>() + p_begin,
+                             (size_t)n * 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(raw.data(), ctx->out_cost_i.as<int32_t>() + p_begin, (size_t)n * 4,
+                             hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+    }
+    for (int i = 0; i < n; ++i) {
+        const bool none = node_out[p_begin + i] < 0;
+        if (cost_out) cost_out[p_begin + i] = none ? 0.f : decode_cost(raw[i], ctx->dtype);
+        if (int_score_out)
+            int_score_out[p_begin + i] = (none || ctx->dtype != NAS_DT_I8)
+                                             ? 0 : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
+    }
+    *stop_out = stop;
+    ctx->timings.commit_ms = tm.total(T_COMMIT);
+    ctx->timings.commit_rounds = hs[2];
     return NAS_OK;
 }
 

@@ -114,6 +114,29 @@ class Engine:
         self._ck(self._L.nas_get_candidate_keys(self._h, ptr(keys), ptr(bounds)))
         return keys, bounds
 
+    # host-driven steps (include/nas.h): score a range, move lists, commit
+    def score_range(self, p_lo, p_hi):
+        self._ck(self._L.nas_score_range(self._h, p_lo, p_hi))
+
+    def candidate_keys_range(self, p_lo, n):
+        keys = np.empty((n, _lib.K_CANDIDATES), np.uint64)
+        bounds = np.empty(n, np.uint64)
+        self._ck(self._L.nas_get_candidate_keys_range(self._h, p_lo, n, ptr(keys), ptr(bounds)))
+        return keys, bounds
+
+    def set_candidate_keys(self, p_lo, keys, bounds):
+        keys = as_c(keys, np.uint64)
+        bounds = as_c(bounds, np.uint64)
+        self._ck(self._L.nas_set_candidate_keys(self._h, p_lo, bounds.shape[0], ptr(keys),
+                                                ptr(bounds)))
+
+    def commit(self, p_begin, node, score=None):
+        """Commit pods [p_begin, P) into node (and score); returns the stop pod."""
+        stop = ctypes.c_int32(0)
+        self._ck(self._L.nas_commit(self._h, p_begin, ptr(node), None, ptr(score),
+                                    ctypes.byref(stop)))
+        return stop.value
+
     @staticmethod
     def comm_unique_id():
         b = (ctypes.c_uint8 * 128)()

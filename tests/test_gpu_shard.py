@@ -60,3 +60,70 @@ def test_shard_rejects_place_and_late_set(engine):
             e.place()
         with pytest.raises(Exception):
             e.set_shard(1, 2)
+
+
+@pytest.mark.parametrize("G,P,N", [(2, 3000, 500), (3, 5000, 700), (4, 2500, 257)])
+def test_host_exchange_place_equals_single_context(G, P, N):
+    """The whole sharded placement (score -> host exchange + merge -> replicated
+    commit -> rescore windows) over G node-shard contexts equals one context's
+    nas_place and the sequential oracle -- placements, scores, capacity."""
+    from kubernetesnetawarescheduler_amd.sharded import place_local_shards
+    rng = np.random.default_rng(G * 7 + P)
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=40, cap_scale=0.15)
+    WA[:, : N // 16] = 127  # crowding: commit conflicts and rescore windows
+    engines = []
+    try:
+        for r in range(G):
+            e = Engine(0)
+            engines.append(e)
+            e.set_shard(r, G)
+            e.upload_latency(L, "i8")
+            e.upload_capacity(free)
+            e.upload_pods(req)
+            e.upload_traffic(WA, "i8")
+        node, score, rounds = place_local_shards(engines, P)
+        caps = [e.get_capacity() for e in engines]
+    finally:
+        for e in engines:
+            e.close()
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    assert rounds > 0
+    assert node.tolist() == want.tolist()
+    assert score.tolist() == wcost.tolist()
+    for c in caps:
+        assert (c == wfree).all()
+    with Engine(0) as e:
+        e.upload_latency(L, "i8")
+        e.upload_capacity(free)
+        e.upload_pods(req)
+        e.upload_traffic(WA, "i8")
+        n1, _, s1 = e.place()
+    assert n1.tolist() == node.tolist() and s1.tolist() == score.tolist()
+
+
+def test_commit_api_stops_and_resumes(engine):
+    """nas_commit on one context: stop pods, rescore windows, resume --
+    equals nas_place."""
+    rng = np.random.default_rng(9)
+    P, N = 4000, 300
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=30, cap_scale=0.1)
+    WA[:, :10] = 127
+    engine.upload_latency(L, "i8")
+    engine.upload_capacity(free)
+    engine.upload_pods(req)
+    engine.upload_traffic(WA, "i8")
+    engine.score_range(0, P)
+    node = np.full(P, -9, np.int32)
+    score = np.zeros(P, np.int64)
+    stop, stops = 0, []
+    while True:
+        stop = engine.commit(stop, node, score)
+        if stop >= P:
+            break
+        stops.append(stop)
+        assert (node[:stop] != -9).all()
+        engine.score_range(stop, min(P, stop + 1024))
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    assert stops and stops == sorted(stops)
+    assert node.tolist() == want.tolist() and score.tolist() == wcost.tolist()
+    assert (engine.get_capacity() == wfree).all()
