@@ -189,6 +189,16 @@ int nas_score(nas_ctx *ctx);
 int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i,
                        float *cand_cost_f, int32_t *count, int32_t *complete);
 
+/* ---- multi-tenant batches (BASELINE config C5) ----------------------------
+ * n_clusters independent clusters of the same shape (nodes, pods, dtype)
+ * placed by one call: every extended-mode array passed to the upload calls,
+ * nas_get_capacity, nas_place and nas_get_candidates then holds the
+ * clusters back to back (cluster b's L at L + b*n*n, its pods at b*P, ...).
+ * Call before the extended uploads; not combinable with node shards, CSR
+ * traffic, nas_filter or the host-driven steps.  Clusters are independent:
+ * each one's placements equal a single-cluster nas_place on its inputs. */
+int nas_set_batch(nas_ctx *ctx, int32_t n_clusters);
+
 /* ---- multi-GPU: node axis sharded over the GPUs of one node ---------------
  * Rank r of `world` owns node columns [r*n/world, (r+1)*n/world) of L; pods,
  * WA and capacities are replicated.  Per-pod candidate lists are exchanged
@@ -256,8 +266,12 @@ int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t
  * concentrated there; capacity and requests per SURVEY.md §8(d) C2/C3. */
 int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, int32_t dtype,
                       int32_t peers);
+/* A batch of n_clusters synthetic clusters; cluster b is the cluster
+ * nas_synth_cluster(seed + b, ...) generates (sets the batch). */
+int nas_synth_batch(nas_ctx *ctx, uint64_t seed, int32_t n_clusters, int32_t n_nodes, int32_t P,
+                    int32_t dtype, int32_t peers);
 /* Read back rows of the device-resident inputs (for sampled oracle checks):
- * WA rows [p0, p0+np), the full L, capacity and requests. */
+ * WA rows [p0, p0+np), the full L, capacity and requests (cluster 0 of a batch). */
 int nas_read_inputs(nas_ctx *ctx, int32_t p0, int32_t np, void *WA_rows, void *L,
                     int32_t *cap_cpu, int32_t *cap_mem, int32_t *cap_pods, int32_t *req_cpu,
                     int32_t *req_mem, int32_t *req_pods);

@@ -90,6 +90,8 @@ SIGNATURES = {
     "nas_synth_snapshots": (_I, [_CTX, _c.c_uint64, _I, _I]),
     "nas_read_snapshot": (_I, [_CTX, _I, _V, _V, _V, _V, _V, _V]),
     "nas_synth_cluster": (_I, [_CTX, _c.c_uint64, _I, _I, _I, _I]),
+    "nas_set_batch": (_I, [_CTX, _I]),
+    "nas_synth_batch": (_I, [_CTX, _c.c_uint64, _I, _I, _I, _I, _I]),
     "nas_read_inputs": (_I, [_CTX, _I, _I, _V, _V, _V, _V, _V, _V, _V, _V]),
 }
 

@@ -63,6 +63,15 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
          const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
          int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
          int *__restrict__ halt) {
+    // one workgroup per cluster of a batched launch
+    const int cb = blockIdx.x;
+    cand_key += (size_t)cb * Pp * KC;
+    cand_bound += (size_t)cb * Pp;
+    req += (size_t)cb * 3 * Pp;
+    cap_g += (size_t)cb * 3 * N;
+    out_node += (size_t)cb * Pp;
+    out_cost += (size_t)cb * Pp;
+    halt += cb * STATUS_INTS;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     __shared__ int first_bad[3];  // round r uses slot r % 3
     __shared__ int s_rescore;     // the round's lowest bad pod needs a rescore
@@ -229,7 +238,7 @@ bool commit_in_lds(int N) { return N <= LDS_CAP_MAX_NODES; }
 
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
-                         int32_t *out_node, int32_t *out_cost, int32_t *halt) {
+                         int32_t *out_node, int32_t *out_cost, int32_t *halt, int batch) {
     if (p_begin >= 0 && p_end <= p_begin) return hipSuccess;
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
@@ -244,10 +253,10 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
             if (e != hipSuccess) return e;
             attr = true;
         }
-        k_commit<true><<<1, THREADS, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
+        k_commit<true><<<batch, THREADS, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
                                                 oc, halt);
     } else {
-        k_commit<false><<<1, THREADS, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
+        k_commit<false><<<batch, THREADS, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
                                                oc, halt);
     }
     return hipGetLastError();

@@ -142,8 +142,14 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     const int gm = min(n_mt - first_mt, GM);
     const int mt = first_mt + (v % gsize) % gm;
     const int nt = (v % gsize) / gm;
+    const int cb = blockIdx.y;  // cluster of a batched launch
+    Lt += (size_t)cb * n_mt * BM * Kb;
+    WA += (size_t)cb * Pp * Kb;
+    mask += (size_t)cb * (n_mt * BM / 64) * Pp;
+    partial += (size_t)cb * n_mt * Pp * KC;
+    pbound += (size_t)cb * n_mt * Pp;
     if (dyn_start) {  // rescore slot: pod tiles from the window start in device memory
-        const int s = *dyn_start;
+        const int s = dyn_start[cb * STATUS_INTS];
         if (s < 0) return;
         p0 = s / BN * BN;
         if (p0 + nt * BN >= dyn_hi) return;  // whole block: before any barrier
@@ -576,9 +582,14 @@ __global__ void __launch_bounds__(256)
 k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_lists,
         long long stride, long long bstride, int src_p0, int p0, int np,
         u64 *__restrict__ dst, u64 *__restrict__ dst_bound, int dst_p0,
-        const int *__restrict__ dyn_start, int dyn_hi, int dyn_flags) {
+        const int *__restrict__ dyn_start, int dyn_hi, int dyn_flags, long long dst_cs) {
+    const int cb = blockIdx.y;  // cluster of a batched launch (dst_cs pods apart)
+    keys += (size_t)cb * n_lists * stride;
+    bounds += (size_t)cb * n_lists * bstride;
+    dst += (size_t)cb * dst_cs * KC;
+    dst_bound += (size_t)cb * dst_cs;
     if (dyn_start) {  // rescore slot: pods [s, min(s + np, hi)); source / destination
-        const int s = *dyn_start;  // indexed from s when flagged (window staging buffers)
+        const int s = dyn_start[cb * STATUS_INTS];  // indexed from s when flagged (staging)
         if (s < 0) return;
         p0 = s;
         np = min(np, dyn_hi - s);
@@ -629,7 +640,7 @@ NAS_INST(0, 0, 4, 4) NAS_INST(1, 0, 4, 4) NAS_INST(0, 0, 4, 8) NAS_INST(0, 0, 4,
 template <int DT>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,
                          int p0, int np, const uint64_t *mask, uint64_t *partial,
-                         uint64_t *pbound, int node_base, const Dyn *dyn) {
+                         uint64_t *pbound, int node_base, const Dyn *dyn, int batch) {
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_cost_topk<DT>),
@@ -639,7 +650,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
         attr_set = true;
     }
     const int n_mt = Mp / BM, n_nt = np / BN;
-    k_cost_topk<DT><<<n_mt * n_nt, THREADS, lds_bytes<COST_PIPE>(), st>>>(
+    k_cost_topk<DT><<<dim3(n_mt * n_nt, batch), THREADS, lds_bytes<COST_PIPE>(), st>>>(
         static_cast<const unsigned char *>(Lt), static_cast<const unsigned char *>(WA), Kb, n_mt,
         n_nt, p0, Pp, reinterpret_cast<const u64 *>(mask), reinterpret_cast<u64 *>(partial),
         reinterpret_cast<u64 *>(pbound), node_base, dyn ? dyn->start : nullptr, dyn ? dyn->hi : 0);
@@ -652,7 +663,8 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
 // p0 + np <= Pp; Mp multiple of BM.
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
-                            uint64_t *partial, uint64_t *pbound, int node_base, const Dyn *dyn) {
+                            uint64_t *partial, uint64_t *pbound, int node_base, const Dyn *dyn,
+                            int batch) {
     if (dyn) {  // tiles covering any window [s, s + win) clipped to hi: one extra for the offset
         p0 = 0;
         np = (int)round_up(dyn->win, BN) + BN;
@@ -663,24 +675,24 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
     if (dtype == NAS_DT_I8) {
         if (Kp % BKB) return hipErrorInvalidValue;
         return launch_cost_t<NAS_DT_I8>(st, Lt, WA, Mp, Kp, Pp, p0, np, mask, partial, pbound,
-                                        node_base, dyn);
+                                        node_base, dyn, batch);
     }
     if ((2 * Kp) % BKB) return hipErrorInvalidValue;
     return launch_cost_t<NAS_DT_BF16>(st, Lt, WA, Mp, 2 * Kp, Pp, p0, np, mask, partial, pbound,
-                                      node_base, dyn);
+                                      node_base, dyn, batch);
 }
 
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0, const Dyn *dyn,
-                        int dyn_flags) {
+                        int dyn_flags, int batch, int64_t dst_cluster_pods) {
     if (dyn) np = dyn->win;
     if (np <= 0) return hipSuccess;
-    k_merge<<<(int)(((int64_t)np * MERGE_LANES + 255) / 256), 256, 0, st>>>(
+    k_merge<<<dim3((int)(((int64_t)np * MERGE_LANES + 255) / 256), batch), 256, 0, st>>>(
         reinterpret_cast<const u64 *>(keys), reinterpret_cast<const u64 *>(bounds), n_lists, stride,
         bstride, src_p0, p0, np, reinterpret_cast<u64 *>(cand_key),
         reinterpret_cast<u64 *>(cand_bound), dst_p0, dyn ? dyn->start : nullptr, dyn ? dyn->hi : 0,
-        dyn_flags);
+        dyn_flags, (long long)dst_cluster_pods);
     return hipGetLastError();
 }
 

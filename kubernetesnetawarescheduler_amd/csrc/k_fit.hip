@@ -32,11 +32,15 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
       const int *__restrict__ req, int Pp, int p0, int p_end, unsigned long long *__restrict__ mask,
       const int *__restrict__ dyn_start, int dyn_win) {
     if (dyn_start) {  // window [*dyn_start, +dyn_win) read from device memory (rescore slots)
-        const int s = *dyn_start;
+        const int s = dyn_start[blockIdx.z * STATUS_INTS];
         if (s < 0) return;
         p0 = s;
         p_end = min(p_end, s + dyn_win);
     }
+    const int cb = blockIdx.z;  // cluster of a batched launch
+    cap += (size_t)cb * 3 * N;
+    req += (size_t)cb * 3 * Pp;
+    mask += (size_t)cb * n_chunks * Pp;
     __shared__ __attribute__((aligned(16))) int sc[3][FIT_CHUNKS * 64];
     const int tid = threadIdx.x;
     const int c0 = blockIdx.y * FIT_CHUNKS;
@@ -83,12 +87,12 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
 
 hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nloc, int Mp,
                       const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask,
-                      const Dyn *dyn) {
+                      const Dyn *dyn, int batch) {
     (void)P;
     if (np <= 0) return hipSuccess;
     const int n_chunks = Mp / 64;
     dim3 grid((np + FIT_THREADS - 1) / FIT_THREADS,
-              (n_chunks + FIT_CHUNKS - 1) / FIT_CHUNKS);
+              (n_chunks + FIT_CHUNKS - 1) / FIT_CHUNKS, batch);
     k_fit<<<grid, FIT_THREADS, 0, st>>>(cap, N, n0, nloc, n_chunks, req, Pp, p0,
                                         dyn ? dyn->hi : p0 + np,
                                         reinterpret_cast<unsigned long long *>(mask),

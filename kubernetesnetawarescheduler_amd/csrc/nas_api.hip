@@ -243,6 +243,14 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     return NAS_OK;
 }
 
+float decode_cost(uint32_t raw, int dtype);
+
+int no_batch(nas_ctx *ctx, const char *what) {
+    if (ctx->B > 1)
+        return nas::fail(ctx, NAS_ERR_UNSUPPORTED, std::string(what) + " with a cluster batch");
+    return NAS_OK;
+}
+
 // A rescore slot on the commit stream, enqueued behind a chunk's commit: if
 // the walk halted at pod s (halt word), rescore pods [s, min(s + RESCORE_PODS,
 // hi)) against the working capacity and resume the walk from s to hi; if it
@@ -253,18 +261,19 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
 int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi) {
     int32_t *halt = ctx->status.as<int32_t>();
     const nas::Dyn dyn{halt, RESCORE_PODS, hi};
+    const int B = ctx->B;  // batched: every cluster with a stop gets its own window
     auto *mask = ctx->mask.as<uint64_t>();
     HIPCK(nas::launch_fit(sc, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
-                          ctx->req.as<int32_t>(), ctx->P, ctx->Pp, 0, RESCORE_PODS, mask, &dyn));
+                          ctx->req.as<int32_t>(), ctx->P, ctx->Pp, 0, RESCORE_PODS, mask, &dyn, B));
     HIPCK(nas::launch_cost_topk(sc, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, ctx->Pp, 0,
                                 0, mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                ctx->Nloc0, &dyn));
+                                ctx->Nloc0, &dyn, B));
     const int n_lists = ctx->Mp / nas::COST_BM;
     if (!exchanging(ctx)) {
         HIPCK(nas::launch_merge(sc, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
                                 n_lists, (int64_t)ctx->Pp * KC, ctx->Pp, 0, 0, 0,
                                 ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(), 0,
-                                &dyn, 0));
+                                &dyn, 0, B, ctx->Pp));
     } else {
         auto *rk = ctx->resc_key.as<uint64_t>();
         auto *rb = ctx->resc_bound.as<uint64_t>();
@@ -281,7 +290,108 @@ int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi) {
     HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), ctx->Pp, -1, hi, ctx->cap.as<int32_t>(),
                              ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
-                             halt));
+                             halt, B));
+    return NAS_OK;
+}
+
+// Scoring pass over every cluster of a batch: one fit, cost/top-k and merge
+// launch each, against the working capacity (cluster = a grid dimension).
+int score_batch(nas_ctx *ctx, Timer &tm) {
+    hipStream_t st = ctx->stream;
+    const int B = ctx->B, P = ctx->P, Pp = ctx->Pp, N = ctx->N;
+    auto *mask = ctx->mask.as<uint64_t>();
+    hipEvent_t e0 = tm.mark(st);
+    HIPCK(nas::launch_fit(st, ctx->cap.as<int32_t>(), N, 0, N, ctx->Mp, ctx->req.as<int32_t>(), P,
+                          Pp, 0, P, mask, nullptr, B));
+    hipEvent_t e1 = tm.mark(st);
+    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, Pp, 0, Pp,
+                                mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), 0,
+                                nullptr, B));
+    hipEvent_t e2 = tm.mark(st);
+    const int n_lists = ctx->Mp / nas::COST_BM;
+    HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
+                            (int64_t)Pp * KC, Pp, 0, 0, P, ctx->cand_key.as<uint64_t>(),
+                            ctx->cand_bound.as<uint64_t>(), 0, nullptr, 0, B, Pp));
+    tm.span(T_FIT, e0, e1);
+    tm.span(T_COST, e1, e2);
+    tm.span(T_MERGE, e2, tm.mark(st));
+    ctx->timings.cost_launches += 1;
+    return NAS_OK;
+}
+
+// Batched placement (B > 1 independent clusters): one fit / cost / merge
+// launch covers every cluster (cluster = a grid dimension), one commit
+// workgroup per cluster walks them in parallel, and batched rescore slots
+// serve every cluster's stop at once until none is left.
+int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
+                int64_t *int_score_out) {
+    hipStream_t st = ctx->stream;
+    const int B = ctx->B, P = ctx->P, Pp = ctx->Pp, N = ctx->N;
+    int32_t *halt = ctx->status.as<int32_t>();
+    int32_t *hs = ctx->host_status.as<int32_t>();
+    hipEvent_t t0 = tm.mark(st);
+    for (int b = 0; b < B; ++b) {
+        hs[b * nas::STATUS_INTS] = -1;
+        for (int j = 1; j < nas::STATUS_INTS; ++j) hs[b * nas::STATUS_INTS + j] = 0;
+    }
+    HIPCK(hipMemcpyAsync(halt, hs, (size_t)B * nas::STATUS_INTS * 4, hipMemcpyHostToDevice, st));
+    OK(score_batch(ctx, tm));
+    hipEvent_t e3 = tm.mark(st);
+    HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                             ctx->req.as<int32_t>(), Pp, 0, P, ctx->cap.as<int32_t>(), N,
+                             ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt, B));
+    for (int r = 0; r < RESCORE_SLOTS_LAST; ++r) OK(rescore_slot(ctx, st, P));
+    tm.span(T_COMMIT, e3, tm.mark(st));
+    int slots = 0;
+    while (true) {
+        HIPCK(hipMemcpyAsync(hs, halt, (size_t)B * nas::STATUS_INTS * 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+        bool any = false;
+        for (int b = 0; b < B; ++b) {
+            const int h = hs[b * nas::STATUS_INTS];
+            if (h >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
+            any |= h >= 0;
+        }
+        if (!any) break;
+        if (++slots > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
+        hipEvent_t c0 = tm.mark(st);
+        OK(rescore_slot(ctx, st, P));
+        tm.span(T_COMMIT, c0, tm.mark(st));
+        ctx->timings.cost_launches += 1;
+    }
+    std::vector<uint32_t> raw;
+    HIPCK(hipMemcpy2DAsync(node_out, (size_t)P * 4, ctx->out_node.p, (size_t)Pp * 4, (size_t)P * 4,
+                           B, hipMemcpyDeviceToHost, st));
+    if (cost_out || int_score_out) {
+        raw.resize((size_t)B * P);
+        HIPCK(hipMemcpy2DAsync(raw.data(), (size_t)P * 4, ctx->out_cost_i.p, (size_t)Pp * 4,
+                               (size_t)P * 4, B, hipMemcpyDeviceToHost, st));
+    }
+    hipEvent_t t1 = tm.mark(st);
+    HIPCK(hipStreamSynchronize(st));
+    tm.span(T_TOTAL, t0, t1);
+    int unsched = 0, dev_rounds = 0, rounds = 0;
+    for (int b = 0; b < B; ++b) {
+        dev_rounds += hs[b * nas::STATUS_INTS + 1];
+        rounds += hs[b * nas::STATUS_INTS + 2];
+    }
+    for (size_t i = 0; i < (size_t)B * P; ++i) {
+        const bool none = node_out[i] < 0;
+        unsched += none;
+        if (cost_out) cost_out[i] = none ? 0.f : decode_cost(raw[i], ctx->dtype);
+        if (int_score_out)
+            int_score_out[i] = (none || ctx->dtype != NAS_DT_I8)
+                                   ? 0 : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
+    }
+    ctx->timings.fit_ms = tm.total(T_FIT);
+    ctx->timings.cost_ms = tm.total(T_COST);
+    ctx->timings.merge_ms = tm.total(T_MERGE);
+    ctx->timings.commit_ms = tm.total(T_COMMIT);
+    ctx->timings.total_ms = tm.total(T_TOTAL);
+    ctx->timings.rescore_rounds = dev_rounds;
+    ctx->timings.unschedulable = unsched;
+    ctx->timings.commit_rounds = rounds;
+    ctx->scored = true;
     return NAS_OK;
 }
 
@@ -307,15 +417,15 @@ int chunk_pods(const nas_ctx *ctx, int c) {
 }
 
 int alloc_extended(nas_ctx *ctx) {
-    const size_t chunks = ctx->Mp / 64;
-    OK(nas::ensure(ctx, ctx->mask, chunks * ctx->Pp * 8));
-    OK(nas::ensure(ctx, ctx->partial, (size_t)(ctx->Mp / nas::COST_BM) * ctx->Pp * KC * 8));
-    OK(nas::ensure(ctx, ctx->pbound, (size_t)(ctx->Mp / nas::COST_BM) * ctx->Pp * 8));
-    OK(nas::ensure(ctx, ctx->cand_key, (size_t)ctx->Pp * KC * 8));
-    OK(nas::ensure(ctx, ctx->cand_bound, (size_t)ctx->Pp * 8));
-    OK(nas::ensure(ctx, ctx->out_node, (size_t)ctx->Pp * 4));
-    OK(nas::ensure(ctx, ctx->out_cost_i, (size_t)ctx->Pp * 4));
-    OK(nas::ensure(ctx, ctx->status, 256));
+    const size_t chunks = ctx->Mp / 64, B = ctx->B;
+    OK(nas::ensure(ctx, ctx->mask, B * chunks * ctx->Pp * 8));
+    OK(nas::ensure(ctx, ctx->partial, B * (ctx->Mp / nas::COST_BM) * ctx->Pp * KC * 8));
+    OK(nas::ensure(ctx, ctx->pbound, B * (ctx->Mp / nas::COST_BM) * ctx->Pp * 8));
+    OK(nas::ensure(ctx, ctx->cand_key, B * ctx->Pp * KC * 8));
+    OK(nas::ensure(ctx, ctx->cand_bound, B * ctx->Pp * 8));
+    OK(nas::ensure(ctx, ctx->out_node, B * ctx->Pp * 4));
+    OK(nas::ensure(ctx, ctx->out_cost_i, B * ctx->Pp * 4));
+    OK(nas::ensure(ctx, ctx->status, std::max<size_t>(256, B * nas::STATUS_INTS * 4)));
     OK(nas::ensure(ctx, ctx->cap_snap, (size_t)3 * ctx->N * 4));
     if (exchanging(ctx)) {
         for (int i = 0; i < 2; ++i) {
@@ -327,9 +437,13 @@ int alloc_extended(nas_ctx *ctx) {
         OK(nas::ensure(ctx, ctx->gather_r, (size_t)ctx->world * RESCORE_PODS * KC * 8));
         OK(nas::ensure(ctx, ctx->gbound_r, (size_t)ctx->world * RESCORE_PODS * 8));
     }
-    if (!ctx->host_status.p) {
-        HIPCK(hipHostMalloc(&ctx->host_status.p, 256, hipHostMallocDefault));
-        ctx->host_status.bytes = 256;
+    const size_t hs_bytes = std::max<size_t>(256, B * nas::STATUS_INTS * 4);
+    if (ctx->host_status.bytes < hs_bytes) {
+        if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
+        ctx->host_status.p = nullptr;
+        ctx->host_status.bytes = 0;
+        HIPCK(hipHostMalloc(&ctx->host_status.p, hs_bytes, hipHostMallocDefault));
+        ctx->host_status.bytes = hs_bytes;
     }
     return NAS_OK;
 }
@@ -503,13 +617,18 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
     set_geometry(ctx, n, dtype);
     if (ctx->have_wa && (ctx->wa_n != n || ctx->wa_dtype != dtype)) ctx->have_wa = false;
     const size_t e = esz(dtype);
-    OK(nas::ensure(ctx, ctx->Lt, (size_t)ctx->Mp * ctx->Kp * e));
+    const size_t lt_b = (size_t)ctx->Mp * ctx->Kp * e;  // one cluster's Lt
+    OK(nas::ensure(ctx, ctx->Lt, lt_b * ctx->B));
     DevBuf tmp;
     OK(nas::ensure(ctx, tmp, (size_t)n * n * e));
-    hipError_t he = hipMemcpyAsync(tmp.p, L, (size_t)n * n * e, hipMemcpyHostToDevice, ctx->stream);
-    if (he == hipSuccess)
-        he = nas::launch_transpose_L(ctx->stream, tmp.p, dtype, n, ctx->Nloc0, ctx->Nloc, ctx->Mp,
-                                     ctx->Kp, ctx->Lt.p);
+    hipError_t he = hipSuccess;
+    for (int b = 0; b < ctx->B && he == hipSuccess; ++b) {
+        he = hipMemcpyAsync(tmp.p, static_cast<const char *>(L) + (size_t)b * n * n * e,
+                            (size_t)n * n * e, hipMemcpyHostToDevice, ctx->stream);
+        if (he == hipSuccess)
+            he = nas::launch_transpose_L(ctx->stream, tmp.p, dtype, n, ctx->Nloc0, ctx->Nloc,
+                                         ctx->Mp, ctx->Kp, ctx->Lt.as<char>() + b * lt_b);
+    }
     if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
     (void)hipFree(tmp.p);
     if (he != hipSuccess) return nas::hip_fail(ctx, he, "upload latency");
@@ -526,13 +645,15 @@ int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *m
     if (!cpu_milli || !mem_kib || !pods || n <= 0)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_capacity");
     if (!ctx->have_L && !ctx->have_wa) set_geometry(ctx, n, ctx->dtype ? ctx->dtype : NAS_DT_I8);
-    OK(nas::ensure(ctx, ctx->cap0, (size_t)3 * n * 4));
-    OK(nas::ensure(ctx, ctx->cap, (size_t)3 * n * 4));
+    const size_t B = ctx->B;
+    OK(nas::ensure(ctx, ctx->cap0, B * 3 * n * 4));
+    OK(nas::ensure(ctx, ctx->cap, B * 3 * n * 4));
     const int32_t *src[3] = {cpu_milli, mem_kib, pods};
-    for (int r = 0; r < 3; ++r)
-        HIPCK(hipMemcpyAsync(ctx->cap0.as<int32_t>() + (size_t)r * n, src[r], (size_t)n * 4,
-                             hipMemcpyHostToDevice, ctx->stream));
-    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * n * 4, hipMemcpyDeviceToDevice,
+    for (size_t b = 0; b < B; ++b)
+        for (int r = 0; r < 3; ++r)
+            HIPCK(hipMemcpyAsync(ctx->cap0.as<int32_t>() + (b * 3 + r) * n, src[r] + b * n,
+                                 (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, B * 3 * n * 4, hipMemcpyDeviceToDevice,
                          ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
     ctx->have_cap = true;
@@ -543,7 +664,7 @@ int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *m
 int nas_reset_capacity(nas_ctx *ctx) {
     OK(bind(ctx));
     if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
-    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * ctx->cap_n * 4,
+    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)ctx->B * 3 * ctx->cap_n * 4,
                          hipMemcpyDeviceToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
     return NAS_OK;
@@ -556,9 +677,10 @@ int nas_get_capacity(nas_ctx *ctx, int32_t *cpu_milli, int32_t *mem_kib, int32_t
     if (n != ctx->cap_n || !cpu_milli || !mem_kib || !pods)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_get_capacity");
     int32_t *dst[3] = {cpu_milli, mem_kib, pods};
-    for (int r = 0; r < 3; ++r)
-        HIPCK(hipMemcpyAsync(dst[r], ctx->cap.as<int32_t>() + (size_t)r * n, (size_t)n * 4,
-                             hipMemcpyDeviceToHost, ctx->stream));
+    for (size_t b = 0; b < (size_t)ctx->B; ++b)
+        for (int r = 0; r < 3; ++r)
+            HIPCK(hipMemcpyAsync(dst[r] + b * n, ctx->cap.as<int32_t>() + (b * 3 + r) * n,
+                                 (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
     return NAS_OK;
 }
@@ -567,14 +689,18 @@ int nas_upload_pods(nas_ctx *ctx, const int32_t *rc, const int32_t *rm, const in
                     int32_t P) {
     OK(bind(ctx));
     if (!rc || !rm || !rp || P <= 0) return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_pods");
-    for (int p = 0; p < P; ++p)
+    const size_t B = ctx->B;
+    for (size_t p = 0; p < B * P; ++p)
         if (rc[p] < 0 || rm[p] < 0 || rp[p] < 0)
             return nas::fail(ctx, NAS_ERR_ARG, "negative resource request");
     const int Pp = (int)nas::round_up(P, nas::COST_BN);
-    std::vector<int32_t> h((size_t)3 * Pp, 0);
-    std::copy(rc, rc + P, h.begin());
-    std::copy(rm, rm + P, h.begin() + Pp);
-    std::copy(rp, rp + P, h.begin() + 2 * (size_t)Pp);
+    std::vector<int32_t> h(B * 3 * Pp, 0);  // [B][3][Pp]
+    for (size_t b = 0; b < B; ++b) {
+        const size_t o = b * 3 * Pp, q = b * P;
+        std::copy(rc + q, rc + q + P, h.begin() + o);
+        std::copy(rm + q, rm + q + P, h.begin() + o + Pp);
+        std::copy(rp + q, rp + q + P, h.begin() + o + 2 * (size_t)Pp);
+    }
     OK(nas::ensure(ctx, ctx->req, h.size() * 4));
     HIPCK(hipMemcpyAsync(ctx->req.p, h.data(), h.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
@@ -596,8 +722,9 @@ static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
     }
     ctx->P = P;
     ctx->Pp = (int32_t)nas::round_up(P, nas::COST_BN);
-    OK(nas::ensure(ctx, ctx->WA, (size_t)ctx->Pp * ctx->Kp * esz(dtype)));
-    HIPCK(hipMemsetAsync(ctx->WA.p, 0, (size_t)ctx->Pp * ctx->Kp * esz(dtype), ctx->stream));
+    const size_t wa_bytes = (size_t)ctx->B * ctx->Pp * ctx->Kp * esz(dtype);
+    OK(nas::ensure(ctx, ctx->WA, wa_bytes));
+    HIPCK(hipMemsetAsync(ctx->WA.p, 0, wa_bytes, ctx->stream));
     ctx->wa_P = P;
     ctx->wa_n = n;
     ctx->wa_dtype = dtype;
@@ -609,8 +736,10 @@ int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_
     if (!WA) return nas::fail(ctx, NAS_ERR_ARG, "WA null");
     OK(traffic_common(ctx, dtype, P, n));
     const size_t e = esz(dtype);
-    HIPCK(hipMemcpy2DAsync(ctx->WA.p, (size_t)ctx->Kp * e, WA, (size_t)n * e, (size_t)n * e, P,
-                           hipMemcpyHostToDevice, ctx->stream));
+    for (size_t b = 0; b < (size_t)ctx->B; ++b)
+        HIPCK(hipMemcpy2DAsync(ctx->WA.as<char>() + b * ctx->Pp * ctx->Kp * e, (size_t)ctx->Kp * e,
+                               static_cast<const char *>(WA) + b * P * n * e, (size_t)n * e,
+                               (size_t)n * e, P, hipMemcpyHostToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
     ctx->have_wa = true;
     ctx->synth_valid = false;
@@ -622,6 +751,7 @@ int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *
     OK(bind(ctx));
     if (!row_ptr || nnz < 0 || (nnz > 0 && (!peer_node || !weight)))
         return nas::fail(ctx, NAS_ERR_ARG, "csr arrays");
+    if (ctx->B > 1) return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "CSR traffic with a cluster batch");
     if (row_ptr[0] != 0 || row_ptr[P] != nnz) return nas::fail(ctx, NAS_ERR_ARG, "row_ptr bounds");
     for (int p = 0; p < P; ++p)
         if (row_ptr[p + 1] < row_ptr[p]) return nas::fail(ctx, NAS_ERR_ARG, "row_ptr not monotone");
@@ -655,6 +785,7 @@ int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *
 
 int nas_filter(nas_ctx *ctx, uint64_t *mask_out) {
     OK(bind(ctx));
+    OK(no_batch(ctx, "nas_filter"));
     if (!ctx->have_cap || !ctx->have_pods || ctx->N <= 0)
         return nas::fail(ctx, NAS_ERR_STATE, "nas_filter needs capacity and pods");
     if (ctx->cap_n != ctx->N || ctx->req_P != ctx->P)
@@ -683,7 +814,8 @@ int nas_score(nas_ctx *ctx) {
     OK(alloc_extended(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
-    OK(score_range(ctx, tm, 0, ctx->P));
+    if (ctx->B > 1) OK(score_batch(ctx, tm));
+    else OK(score_range(ctx, tm, 0, ctx->P));
     HIPCK(hipStreamSynchronize(ctx->stream));
     ctx->timings.fit_ms = tm.total(T_FIT);
     ctx->timings.cost_ms = tm.total(T_COST);
@@ -702,6 +834,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     OK(alloc_extended(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
+    if (ctx->B > 1) return place_batch(ctx, tm, node_out, cost_out, int_score_out);
     hipStream_t st = ctx->stream, sc = ctx->stream_commit;
     const int P = ctx->P, N = ctx->N;
     int32_t *halt = ctx->status.as<int32_t>();
@@ -795,14 +928,15 @@ int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i, f
                        int32_t *count, int32_t *complete) {
     OK(bind(ctx));
     if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
-    const int P = ctx->P;
+    const int64_t P = (int64_t)ctx->B * ctx->P;  // a batch: B clusters back to back
     std::vector<uint64_t> keys((size_t)P * KC), bounds(P);
-    HIPCK(hipMemcpyAsync(keys.data(), ctx->cand_key.p, keys.size() * 8, hipMemcpyDeviceToHost,
-                         ctx->stream));
-    HIPCK(hipMemcpyAsync(bounds.data(), ctx->cand_bound.p, bounds.size() * 8, hipMemcpyDeviceToHost,
-                         ctx->stream));
+    HIPCK(hipMemcpy2DAsync(keys.data(), (size_t)ctx->P * KC * 8, ctx->cand_key.p,
+                           (size_t)ctx->Pp * KC * 8, (size_t)ctx->P * KC * 8, ctx->B,
+                           hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipMemcpy2DAsync(bounds.data(), (size_t)ctx->P * 8, ctx->cand_bound.p, (size_t)ctx->Pp * 8,
+                           (size_t)ctx->P * 8, ctx->B, hipMemcpyDeviceToHost, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
-    for (int p = 0; p < P; ++p) {
+    for (int64_t p = 0; p < P; ++p) {
         int c = 0;
         for (int j = 0; j < KC; ++j) {
             const uint64_t k = keys[(size_t)p * KC + j];
@@ -824,6 +958,7 @@ int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i, f
 // ------------------------------------------------------- host-driven steps
 int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi) {
     OK(bind(ctx));
+    OK(no_batch(ctx, "nas_score_range"));
     OK(check_extended(ctx));
     if (p_lo < 0 || p_hi > ctx->P || p_lo >= p_hi)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_score_range: pod range");
@@ -850,6 +985,7 @@ static int keys_range_ok(nas_ctx *ctx, int32_t p_lo, int32_t n, const void *keys
 int nas_get_candidate_keys_range(nas_ctx *ctx, int32_t p_lo, int32_t n, uint64_t *keys,
                                  uint64_t *bounds) {
     OK(bind(ctx));
+    OK(no_batch(ctx, "candidate key ranges"));
     OK(keys_range_ok(ctx, p_lo, n, keys, bounds));
     if (n == 0) return NAS_OK;
     HIPCK(hipMemcpyAsync(keys, ctx->cand_key.as<uint64_t>() + (size_t)p_lo * KC, (size_t)n * KC * 8,
@@ -863,6 +999,7 @@ int nas_get_candidate_keys_range(nas_ctx *ctx, int32_t p_lo, int32_t n, uint64_t
 int nas_set_candidate_keys(nas_ctx *ctx, int32_t p_lo, int32_t n, const uint64_t *keys,
                            const uint64_t *bounds) {
     OK(bind(ctx));
+    OK(no_batch(ctx, "candidate key ranges"));
     OK(keys_range_ok(ctx, p_lo, n, keys, bounds));
     // the commit relies on sorted lists with in-range node ids
     for (int64_t i = 0; i < (int64_t)n; ++i) {
@@ -887,6 +1024,7 @@ int nas_set_candidate_keys(nas_ctx *ctx, int32_t p_lo, int32_t n, const uint64_t
 int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out,
                int64_t *int_score_out, int32_t *stop_out) {
     OK(bind(ctx));
+    OK(no_batch(ctx, "nas_commit"));
     OK(check_extended(ctx));
     if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "nas_commit needs candidate lists");
     if (!node_out || !stop_out || p_begin < 0 || p_begin > ctx->P)
@@ -949,6 +1087,8 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
         return nas::fail(ctx, NAS_ERR_ARG, "nas_comm_init: rank/world");
     if (ctx->have_L || ctx->have_wa || ctx->have_cap)
         return nas::fail(ctx, NAS_ERR_STATE, "nas_comm_init must precede the extended uploads");
+    if (ctx->B > 1 && world > 1)
+        return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");
     destroy_comms(ctx);
     ctx->rank = rank;
     ctx->world = world;
@@ -981,6 +1121,8 @@ int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world) {
     if (ctx->comm) return nas::fail(ctx, NAS_ERR_STATE, "context already has a communicator");
     if (ctx->have_L || ctx->have_wa || ctx->have_cap)
         return nas::fail(ctx, NAS_ERR_STATE, "nas_set_shard must precede the extended uploads");
+    if (ctx->B > 1 && world > 1)
+        return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");
     ctx->rank = rank;
     ctx->world = world;
     ctx->virtual_shard = world > 1;
@@ -989,6 +1131,7 @@ int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world) {
 
 int nas_get_candidate_keys(nas_ctx *ctx, uint64_t *keys, uint64_t *bounds) {
     OK(bind(ctx));
+    OK(no_batch(ctx, "nas_get_candidate_keys"));
     if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
     if (keys)
         HIPCK(hipMemcpyAsync(keys, ctx->cand_key.p, (size_t)ctx->P * KC * 8, hipMemcpyDeviceToHost,
@@ -1032,26 +1175,44 @@ int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t
     return NAS_OK;
 }
 
-int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, int32_t dtype,
-                      int32_t peers) {
+int nas_set_batch(nas_ctx *ctx, int32_t n_clusters) {
     OK(bind(ctx));
-    if (n_nodes <= 0 || P <= 0 || peers < 1 || peers > 16 ||
+    if (n_clusters < 1 || n_clusters > 65535)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_set_batch: n_clusters");
+    if (ctx->have_L || ctx->have_wa || ctx->have_cap || ctx->have_pods)
+        return nas::fail(ctx, NAS_ERR_STATE, "nas_set_batch must precede the extended uploads");
+    if (ctx->world > 1 && n_clusters > 1)
+        return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");
+    ctx->B = n_clusters;
+    return NAS_OK;
+}
+
+static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_t P,
+                 int32_t dtype, int32_t peers) {
+    if (n_nodes <= 0 || P <= 0 || peers < 1 || peers > 16 || B < 1 ||
         (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
         return nas::fail(ctx, NAS_ERR_ARG, "nas_synth_cluster arguments");
+    if (B > 1 && ctx->world > 1)
+        return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");
+    ctx->B = B;
     set_geometry(ctx, n_nodes, dtype);
     ctx->P = P;
     ctx->Pp = (int32_t)nas::round_up(P, nas::COST_BN);
     const size_t e = esz(dtype);
-    OK(nas::ensure(ctx, ctx->Lt, (size_t)ctx->Mp * ctx->Kp * e));
-    OK(nas::ensure(ctx, ctx->WA, (size_t)ctx->Pp * ctx->Kp * e));
-    OK(nas::ensure(ctx, ctx->cap0, (size_t)3 * n_nodes * 4));
-    OK(nas::ensure(ctx, ctx->cap, (size_t)3 * n_nodes * 4));
-    OK(nas::ensure(ctx, ctx->req, (size_t)3 * ctx->Pp * 4));
-    HIPCK(nas::launch_synth_cluster(ctx->stream, seed, n_nodes, P, dtype, peers, ctx->Nloc0,
-                                    ctx->Nloc, ctx->Mp, ctx->Kp, ctx->Pp, ctx->Lt.p, ctx->WA.p,
-                                    ctx->cap0.as<int32_t>(), ctx->req.as<int32_t>(), nullptr));
-    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)3 * n_nodes * 4, hipMemcpyDeviceToDevice,
-                         ctx->stream));
+    const size_t lt_b = (size_t)ctx->Mp * ctx->Kp * e, wa_b = (size_t)ctx->Pp * ctx->Kp * e;
+    OK(nas::ensure(ctx, ctx->Lt, lt_b * B));
+    OK(nas::ensure(ctx, ctx->WA, wa_b * B));
+    OK(nas::ensure(ctx, ctx->cap0, (size_t)B * 3 * n_nodes * 4));
+    OK(nas::ensure(ctx, ctx->cap, (size_t)B * 3 * n_nodes * 4));
+    OK(nas::ensure(ctx, ctx->req, (size_t)B * 3 * ctx->Pp * 4));
+    for (int b = 0; b < B; ++b)  // cluster b is the single cluster of seed + b
+        HIPCK(nas::launch_synth_cluster(ctx->stream, seed + b, n_nodes, P, dtype, peers,
+                                        ctx->Nloc0, ctx->Nloc, ctx->Mp, ctx->Kp, ctx->Pp,
+                                        ctx->Lt.as<char>() + b * lt_b, ctx->WA.as<char>() + b * wa_b,
+                                        ctx->cap0.as<int32_t>() + (size_t)b * 3 * n_nodes,
+                                        ctx->req.as<int32_t>() + (size_t)b * 3 * ctx->Pp, nullptr));
+    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)B * 3 * n_nodes * 4,
+                         hipMemcpyDeviceToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
     ctx->have_L = ctx->have_cap = ctx->have_pods = ctx->have_wa = true;
     ctx->L_n = ctx->cap_n = ctx->wa_n = n_nodes;
@@ -1060,6 +1221,18 @@ int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, i
     ctx->synth_valid = true;
     ctx->synth_seed = seed;
     return NAS_OK;
+}
+
+int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, int32_t dtype,
+                      int32_t peers) {
+    OK(bind(ctx));
+    return synth(ctx, seed, 1, n_nodes, P, dtype, peers);
+}
+
+int nas_synth_batch(nas_ctx *ctx, uint64_t seed, int32_t n_clusters, int32_t n_nodes, int32_t P,
+                    int32_t dtype, int32_t peers) {
+    OK(bind(ctx));
+    return synth(ctx, seed, n_clusters, n_nodes, P, dtype, peers);
 }
 
 int nas_read_inputs(nas_ctx *ctx, int32_t p0, int32_t np, void *WA_rows, void *L, int32_t *cap_cpu,

@@ -31,6 +31,10 @@ struct DevBuf {
     T *as() const { return static_cast<T *>(p); }
 };
 
+// per-cluster commit control words in ctx->status: halt (pod to rescore or
+// -1), device-side rescores, commit rounds, spare
+constexpr int STATUS_INTS = 4;
+
 // packed candidate key: orderable 32-bit cost in the high word, node index
 // in the low word; ascending key == ascending (cost, node).
 constexpr uint64_t KEY_INVALID = ~0ull;
@@ -65,6 +69,8 @@ struct nas_ctx {
     int32_t Nloc0 = 0, Nloc = 0;  // node shard [Nloc0, Nloc0+Nloc) owned by this rank
     int32_t Mp = 0;          // padded local node count (multiple of COST_BM)
     int32_t Pp = 0;          // padded pod count (multiple of COST_BN)
+    int32_t B = 1;           // independent clusters of equal shape (nas_set_batch)
+    int32_t cur_cluster = 0; // target of per-cluster uploads / reads (nas_select_cluster)
     bool have_L = false, have_cap = false, have_pods = false, have_wa = false;
     int32_t L_n = 0, L_dtype = 0, cap_n = 0, req_P = 0, wa_P = 0, wa_n = 0, wa_dtype = 0;
     nas::DevBuf Lt;          // [Mp][Kp] elements: Lt[i][m] = L[m][Nloc0 + i]
@@ -112,6 +118,9 @@ hipError_t launch_vote_gather(hipStream_t st, const int32_t *pod_snap, int P,
 // A rescore slot's pod window, decided on the device: the kernels read the
 // window start from *start (the commit's halt word; < 0 = nothing to do) and
 // cover pods [start, min(start + win, hi)).  Grids are sized for `win`.
+// Batched launches (batch > 1 independent clusters of equal shape, laid out
+// back to back; the cluster index is a grid dimension) read cluster b's
+// start at start[b * STATUS_INTS].
 struct Dyn {
     const int32_t *start;
     int win;
@@ -122,22 +131,23 @@ constexpr int MERGE_DST_WINDOW = 2;  // k_merge destination indexed from the win
 
 hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nloc, int Mp,
                       const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask,
-                      const Dyn *dyn = nullptr);
+                      const Dyn *dyn = nullptr, int batch = 1);
 
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base,
-                            const Dyn *dyn = nullptr);
+                            const Dyn *dyn = nullptr, int batch = 1);
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,
-                        const Dyn *dyn = nullptr, int dyn_flags = 0);
+                        const Dyn *dyn = nullptr, int dyn_flags = 0, int batch = 1,
+                        int64_t dst_cluster_pods = 0);
 // the commit keeps the working capacity in LDS (and publishes only final
 // values, at the end of each launch) for clusters of up to this many nodes
 bool commit_in_lds(int N);
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
-                         int32_t *out_node, int32_t *out_cost_i, int32_t *halt);
+                         int32_t *out_node, int32_t *out_cost_i, int32_t *halt, int batch = 1);
 
 hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
                               int nloc, int Mp, int Kp, void *Lt);

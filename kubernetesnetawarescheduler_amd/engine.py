@@ -29,6 +29,7 @@ class Engine:
         self.n_nodes = 0
         self.n_pods = 0
         self.dtype = 0
+        self.n_clusters = 1  # nas_set_batch: arrays carry a leading cluster axis when > 1
 
     # ------------------------------------------------------------ plumbing
     def _ck(self, rc):
@@ -153,36 +154,53 @@ class Engine:
     def _np(dtype):
         return np.int8 if dtype == "i8" else np.uint16
 
+    # A batch (set_batch / synth_batch) passes every extended-mode array with a
+    # leading cluster axis: L (B, n, n), free (B, n, 3), req (B, P, 3), WA (B, P, n).
+    def set_batch(self, n_clusters):
+        self._ck(self._L.nas_set_batch(self._h, n_clusters))
+        self.n_clusters = n_clusters
+
+    def synth_batch(self, seed, n_clusters, n_nodes, P, dtype="i8", peers=8):
+        self._ck(self._L.nas_synth_batch(self._h, seed, n_clusters, n_nodes, P, self._dt(dtype),
+                                         peers))
+        self.n_clusters, self.n_nodes, self.n_pods, self.dtype = n_clusters, n_nodes, P, dtype
+
+    @staticmethod
+    def _cols(a, last):
+        """(..., last) array -> `last` contiguous columns over every cluster."""
+        return [np.ascontiguousarray(a[..., i]).reshape(-1) for i in range(last)]
+
     def upload_latency(self, L, dtype):
         L = as_c(L, self._np(dtype))
-        n = L.shape[0]
+        n = L.shape[-1]
         self._ck(self._L.nas_upload_latency(self._h, ptr(L), self._dt(dtype), n))
         self.n_nodes, self.dtype = n, dtype
 
     def upload_capacity(self, free):
         free = as_c(free, np.int32)
-        cols = [np.ascontiguousarray(free[:, i]) for i in range(3)]
-        self._ck(self._L.nas_upload_capacity(self._h, *[ptr(c) for c in cols], free.shape[0]))
-        self.n_nodes = free.shape[0]
+        cols = self._cols(free, 3)
+        self._ck(self._L.nas_upload_capacity(self._h, *[ptr(c) for c in cols], free.shape[-2]))
+        self.n_nodes = free.shape[-2]
 
     def reset_capacity(self):
         self._ck(self._L.nas_reset_capacity(self._h))
 
     def get_capacity(self):
-        n = self.n_nodes
-        cols = [np.empty(n, np.int32) for _ in range(3)]
+        n, B = self.n_nodes, self.n_clusters
+        cols = [np.empty(B * n, np.int32) for _ in range(3)]
         self._ck(self._L.nas_get_capacity(self._h, *[ptr(c) for c in cols], n))
-        return np.stack(cols, axis=1)
+        out = np.stack(cols, axis=1)
+        return out if B == 1 else out.reshape(B, n, 3)
 
     def upload_pods(self, req):
         req = as_c(req, np.int32)
-        cols = [np.ascontiguousarray(req[:, i]) for i in range(3)]
-        self._ck(self._L.nas_upload_pods(self._h, *[ptr(c) for c in cols], req.shape[0]))
-        self.n_pods = req.shape[0]
+        cols = self._cols(req, 3)
+        self._ck(self._L.nas_upload_pods(self._h, *[ptr(c) for c in cols], req.shape[-2]))
+        self.n_pods = req.shape[-2]
 
     def upload_traffic(self, WA, dtype):
         WA = as_c(WA, self._np(dtype))
-        P, n = WA.shape
+        P, n = WA.shape[-2:]
         self._ck(self._L.nas_upload_traffic_dense(self._h, ptr(WA), self._dt(dtype), P, n))
         self.n_pods, self.n_nodes, self.dtype = P, n, dtype
 
@@ -205,7 +223,7 @@ class Engine:
         self._ck(self._L.nas_score(self._h))
 
     def candidates(self):
-        P, K = self.n_pods, _lib.K_CANDIDATES
+        P, K = self.n_pods * self.n_clusters, _lib.K_CANDIDATES
         node = np.empty((P, K), np.int32)
         ci = np.empty((P, K), np.int64)
         cf = np.empty((P, K), np.float32)
@@ -216,11 +234,15 @@ class Engine:
         return node, ci, cf, cnt, complete.astype(bool)
 
     def place(self, want_cost=True):
-        P = self.n_pods
-        node = np.empty(P, np.int32)
-        cf = np.empty(P, np.float32) if want_cost else None
-        ci = np.empty(P, np.int64) if want_cost else None
+        B, P = self.n_clusters, self.n_pods
+        node = np.empty(B * P, np.int32)
+        cf = np.empty(B * P, np.float32) if want_cost else None
+        ci = np.empty(B * P, np.int64) if want_cost else None
         self._ck(self._L.nas_place(self._h, ptr(node), ptr(cf), ptr(ci)))
+        if B > 1:
+            node = node.reshape(B, P)
+            cf = None if cf is None else cf.reshape(B, P)
+            ci = None if ci is None else ci.reshape(B, P)
         return node, cf, ci
 
     def synth_cluster(self, seed, n_nodes, P, dtype="i8", peers=8):
