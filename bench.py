@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--no-reference-mode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the other BASELINE configs (C1/C2/C5 lines under 'configs')")
+    ap.add_argument("--c4", action="store_true",
+                    help="also run C4 (50k nodes x 500k pods) on this GPU count")
     ap.add_argument("--only", choices=["place", "vote", "score"], default=None,
                     help="profile helper: run only one path")
     return ap.parse_args()
@@ -224,6 +228,107 @@ def cpu_baseline_vote(args, eng, ref):
             "gpu_matches_oracle_on_sample": bool(ok)}
 
 
+def _timed_place(d, eng, steps, warmup):
+    res = {}
+
+    def step():
+        eng.reset_capacity()
+        res["node"], _, res["score"] = eng.place(want_cost=True)
+        res["t"] = eng.timings()
+
+    return time_steps(d, step, steps, warmup), res
+
+
+def config_c1(args, d, eng):
+    """configs[0]: the reference's own CPU-sized case, ~10 nodes x 100 pods,
+    reference-mode vote scoring (one snapshot per pod), checked against the
+    oracle's literal restatement of scheduler.go:250-394."""
+    import oracle
+    N, S = 10, 100
+    eng.synth_snapshots(SEED, N, S)
+    rng = np.random.default_rng(SEED)
+    o1, o2 = rng.permutation(N).astype(np.int32), rng.permutation(N + 1).astype(np.int32)
+    eng.upload_orders(o1, o2)
+    t = time_steps(d, lambda: eng.score_reference(S), args.steps, args.warmup)
+    best, win = eng.score_reference(S)
+    ok = True
+    for s in range(S):
+        b, w, _ = oracle.vote(eng.read_snapshot(s), o1, o2)
+        ok &= b == best[s] and list(w) == win[s].tolist()
+    return {"workload": f"C1: reference-mode vote, {N} nodes x {S} pods (one snapshot per pod)",
+            "value": S * N / (t / args.steps), "unit": "pair-scores/s",
+            "ms_per_step": t * 1e3 / args.steps, "matches_oracle": bool(ok),
+            "note": "launch-latency bound: one score_reference call per step"}
+
+
+def config_c2(args, d, eng):
+    """configs[1]: clusterloader2-derived 1k x 10k, sparse (CSR) pod
+    communication graph; the whole placement is checked against the oracle."""
+    import oracle
+    from kubernetesnetawarescheduler_amd import workloads
+    N, P = 1000, 10000
+    c = workloads.c2_cluster(SEED, N, P)
+    eng.upload_latency(c["L"], "i8")
+    eng.upload_capacity(c["free"])
+    eng.upload_pods(c["req"])
+    eng.upload_traffic_csr(c["row_ptr"], c["peer_node"], c["weight"], "i8", N)
+    t, res = _timed_place(d, eng, args.steps, args.warmup)
+    WA = workloads.csr_to_dense(c["row_ptr"], c["peer_node"], c["weight"], N)
+    want, wcost, wfree = oracle.place(WA, c["L"], c["req"], c["free"], "i8")
+    ok = (res["node"] == want).all() and (res["score"] == wcost).all() \
+        and (eng.get_capacity() == wfree).all()
+    ms = t * 1e3 / args.steps
+    return {"workload": f"C2: clusterloader2 requests, {N} nodes x {P} pods, CSR traffic "
+                        f"({len(c['peer_node'])} nnz), latency U[50,500] us in 4-us int8 steps",
+            "value": P * N / (ms * 1e-3), "unit": "pair-scores/s", "ms_per_step": ms,
+            "placements_per_s": P / (ms * 1e-3), "unschedulable": res["t"]["unschedulable"],
+            "matches_oracle": bool(ok), "oracle_check": f"all {P} pods, scores and capacity"}
+
+
+def config_c5(args, d, eng, B=64, N=5000, P=5000, sample=1024):
+    """configs[4]: 64 independent 5k-node clusters (5k pending pods each) in
+    one batched nas_place; cluster 0's first `sample` pods checked against the
+    oracle (sequential greedy over a prefix depends only on that prefix)."""
+    import oracle
+    eng.synth_batch(SEED, B, N, P, "i8", peers=args.peers)
+    t, res = _timed_place(d, eng, args.steps, args.warmup)
+    WA, L, cap, req = eng.read_inputs(0, sample, want_L=True)
+    want, wcost, _ = oracle.place(WA, L, req[:sample], cap, "i8")
+    ok = (res["node"][0, :sample] == want).all() and (res["score"][0, :sample] == wcost).all()
+    ms = t * 1e3 / args.steps
+    return {"workload": f"C5: batch of {B} clusters x {N} nodes x {P} pods (synthetic, seeded)",
+            "value": B * P * N / (ms * 1e-3), "unit": "pair-scores/s", "ms_per_step": ms,
+            "placements_per_s": B * P / (ms * 1e-3), "unschedulable": res["t"]["unschedulable"],
+            "rescore_rounds": res["t"]["rescore_rounds"], "matches_oracle": bool(ok),
+            "oracle_check": f"cluster 0, first {sample} pods"}
+
+
+def config_c4(args, d, eng, N=50000, P=500000):
+    """configs[3]: 50k nodes x 500k pods, node axis sharded over the ranks."""
+    if d.world > 1:
+        uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
+        eng.comm_init(uid, d.rank, d.world)
+    eng.synth_cluster(SEED, N, P, "i8", peers=args.peers)
+    steps = max(1, min(args.steps, 2))
+    t, res = _timed_place(d, eng, steps, 1)
+    ms = t * 1e3 / steps
+    return {"workload": f"C4: {N} nodes x {P} pods, node-sharded x{d.world}",
+            "value": P * N / (ms * 1e-3), "unit": "pair-scores/s", "ms_per_step": ms,
+            "steps": steps, "placements_per_s": P / (ms * 1e-3),
+            "unschedulable": res["t"]["unschedulable"], "rescore_rounds": res["t"]["rescore_rounds"],
+            "stages_ms": {k: res["t"][k] for k in ("fit_ms", "cost_ms", "merge_ms", "commit_ms")}}
+
+
+def run_configs(args, d):
+    """The other BASELINE configs, each on a fresh context (rank 0, one GPU)."""
+    from kubernetesnetawarescheduler_amd import Engine
+    out = {}
+    for name, fn in (("C1", config_c1), ("C2", config_c2), ("C5", config_c5)):
+        with Engine(d.local) as e:
+            out[name] = fn(args, d, e)
+    return out
+
+
 def main():
     args = parse()
     d = Dist(args.gpus)
@@ -287,6 +392,12 @@ def main():
         eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
         out["cpu_baseline"] = cpu_baseline_place(args, eng, gpu_nodes)
     eng.close()
+    if d.world == 1 and not args.no_configs and args.only is None:
+        out["configs"] = run_configs(args, d)
+    if args.c4:
+        from kubernetesnetawarescheduler_amd import Engine
+        with Engine(d.local) as e:
+            out.setdefault("configs", {})["C4"] = config_c4(args, d, e)
     if d.rank == 0:
         print(json.dumps(out), flush=True)
 

@@ -89,6 +89,7 @@ typedef struct nas_timings {
     int32_t rescore_rounds;  /* commit stops that needed a rescore */
     int32_t unschedulable;   /* pods with no fitting node */
     int32_t commit_rounds;   /* rounds of the parallel commit walk (all windows) */
+    int32_t rescored_pods;   /* pods re-scored by host-side gathered rescores */
 } nas_timings;
 
 /* ---- lifecycle --------------------------------------------------------- */

@@ -47,7 +47,8 @@ class NasTimings(ctypes.Structure):
                 ("merge_ms", ctypes.c_float), ("commit_ms", ctypes.c_float),
                 ("vote_ms", ctypes.c_float), ("total_ms", ctypes.c_float),
                 ("cost_launches", ctypes.c_int32), ("rescore_rounds", ctypes.c_int32),
-                ("unschedulable", ctypes.c_int32), ("commit_rounds", ctypes.c_int32)]
+                ("unschedulable", ctypes.c_int32), ("commit_rounds", ctypes.c_int32),
+                ("rescored_pods", ctypes.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

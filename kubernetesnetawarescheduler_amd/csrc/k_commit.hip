@@ -34,6 +34,9 @@
 // halts the launch (halt word) after the pods below it commit; a launch with
 // p_begin < 0 resumes from the halted pod after a rescore slot (nas_api.hip).
 // The working capacity lives in LDS (3 x N int32) when it fits, else in L2.
+// The L2 form's speculative reservations can dip below the committed state, so
+// it also subtracts each committed pod from `pub` (when given): a published
+// capacity that is always >= the working one, for concurrent scoring to read.
 #include "klist.h"
 
 namespace nas {
@@ -62,7 +65,7 @@ __global__ void __launch_bounds__(THREADS)
 k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
          const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
          int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
-         int *__restrict__ halt) {
+         int *__restrict__ halt, int *__restrict__ pub) {
     // one workgroup per cluster of a batched launch
     const int cb = blockIdx.x;
     cand_key += (size_t)cb * Pp * KC;
@@ -72,6 +75,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     out_node += (size_t)cb * Pp;
     out_cost += (size_t)cb * Pp;
     halt += cb * STATUS_INTS;
+    if (pub) pub += (size_t)cb * 3 * N;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     __shared__ int first_bad[3];  // round r uses slot r % 3
     __shared__ int s_rescore;     // the round's lowest bad pod needs a rescore
@@ -114,6 +118,12 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         c.r0 = r0;
         c.r1 = r1;
         c.r2 = r2;
+    };
+    auto publish = [&](int n, const Pod &c) {
+        if (LDS_CAP || !pub || n < 0) return;
+        atomicSub(pub + n, c.r0);
+        atomicSub(pub + N + n, c.r1);
+        atomicSub(pub + 2 * N + n, c.r2);
     };
     auto ld = [&](int idx) -> int {
         if (LDS_CAP) return cap[idx];
@@ -179,6 +189,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 if (!done) {
                     out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
                     out_cost[i] = ccost;
+                    publish(choice, cur);
                 }
                 break;
             }
@@ -191,6 +202,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             if (!done && i < s) {
                 out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
                 out_cost[i] = ccost;
+                publish(choice, cur);
                 done = true;
             }
             if (i == s) s_rescore = rescore;
@@ -212,6 +224,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                     }
                     out_node[i] = n;
                     out_cost[i] = ccost;
+                    publish(n, cur);
                     done = true;
                 }
             }
@@ -238,7 +251,8 @@ bool commit_in_lds(int N) { return N <= LDS_CAP_MAX_NODES; }
 
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
-                         int32_t *out_node, int32_t *out_cost, int32_t *halt, int batch) {
+                         int32_t *out_node, int32_t *out_cost, int32_t *halt, int batch,
+                         int32_t *pub) {
     if (p_begin >= 0 && p_end <= p_begin) return hipSuccess;
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
@@ -254,10 +268,10 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
             attr = true;
         }
         k_commit<true><<<batch, THREADS, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
-                                                oc, halt);
+                                                oc, halt, nullptr);
     } else {
         k_commit<false><<<batch, THREADS, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
-                                               oc, halt);
+                                               oc, halt, pub);
     }
     return hipGetLastError();
 }

@@ -129,7 +129,8 @@ __global__ void k_synth_snap(unsigned long long seed, int n, long long ns, int S
 // Extended-mode cluster (build-defined):
 // nodes in racks of 32, racks in zones of 16; symmetric latency by distance
 // class (0 self, 2-4 same rack, 12-19 same zone, 40-105 cross zone);
-// traffic: dense background 0..2 to every node plus `peers` heavy bound peers
+// traffic: dense background 0..2 to every node (thinned past 10k nodes, see
+// k_synth_bg) plus `peers` heavy bound peers
 // (16..127) in the pod's home rack / zone, saturated at 127;
 // capacity cpu {4000, 8000} m, memory {4, 8} GiB, 110 pods; requests
 // log-uniform over the clusterloader2 ranges (cpu 0.000213-0.5376 cores, mem
@@ -162,7 +163,11 @@ __device__ __forceinline__ int to_int<unsigned short>(unsigned short v) {
 }
 
 // dense background traffic 0..2 to every node (every pod talks a little to
-// everything: the contraction is genuinely dense), zero padding past N
+// everything: the contraction is genuinely dense), zero padding past N.
+// Clusters larger than BG_NODES thin it out so that it does not swamp the
+// peer traffic (at 50k nodes a full background would be ~50 GB per pod
+// against ~0.6 GB to its peers, and every pod would rank nodes alike).
+constexpr int BG_NODES = 10000;
 template <typename T>
 __global__ void k_synth_bg(unsigned long long seed, int N, int P, int Kp, long long total,
                            T *__restrict__ WA) {
@@ -170,7 +175,14 @@ __global__ void k_synth_bg(unsigned long long seed, int N, int P, int Kp, long l
          t += (long long)gridDim.x * blockDim.x) {
         const int p = (int)(t / Kp), m = (int)(t - (long long)p * Kp);
         int v = 0;
-        if (p < P && m < N) v = (int)(mix64(seed ^ ((unsigned long long)t * 0x9e3779b97f4a7c15ull)) % 3);
+        if (p < P && m < N) {
+            const unsigned long long h = mix64(seed ^ ((unsigned long long)t * 0x9e3779b97f4a7c15ull));
+            // past BG_NODES nodes each entry is kept with probability
+            // BG_NODES / N: a pod's total background volume stays that of a
+            // BG_NODES-node cluster instead of growing with N
+            const bool keep = N <= BG_NODES || (int)((h >> 32) % (unsigned)N) < BG_NODES;
+            v = keep ? (int)(h % 3) : 0;
+        }
         WA[t] = from_int<T>(v);
     }
 }
@@ -211,14 +223,14 @@ __global__ void k_synth_pods(unsigned long long seed, int N, int P, int peers, i
     const int np = min(peers, 16);
     for (int j = 0; j < np; ++j) {
         const unsigned long long h = hsh(seed, p, j + 1, 12);
-        int node;
-        if (j < np - 2 || np <= 2) {
-            node = rack * 32 + (int)(h % 32);
-        } else {  // another rack of the same zone
+        // uniform over the racks of the zone and the nodes of the rack (the
+        // last zone / rack may be partial)
+        int r = rack;
+        if (!(j < np - 2 || np <= 2)) {  // another rack of the same zone
             const int zone0 = (rack >> 4) << 4;
-            const int r2 = min(zone0 + (int)((h >> 20) % 16), n_racks - 1);
-            node = r2 * 32 + (int)(h % 32);
+            r = zone0 + (int)((h >> 20) % (unsigned)min(16, n_racks - zone0));
         }
+        const int node = r * 32 + (int)(h % (unsigned)min(32, N - r * 32));
         nodes[j] = min(node, N - 1);
         wts[j] = 16 + (int)((h >> 40) % 112);
     }

@@ -61,7 +61,8 @@ int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes) {
 
 namespace {
 
-constexpr int RESCORE_PODS = 1024;  // pods rescored per commit stop (multiple of COST_BN)
+constexpr int RESCORE_PODS = 1024;  // pods per device-side rescore slot (multiple of COST_BN)
+constexpr int GATHER_PODS = 4096;   // dry pods rescored per host-side stop (rescore_gathered)
 // Device-side rescore slots enqueued behind a chunk's commit.  An idle slot
 // still costs its launches a wait for free CUs while scoring fills the chip,
 // and scoring against the live capacity makes stops rare, so by default only
@@ -201,45 +202,93 @@ int exchange(nas_ctx *ctx, ncclComm *cm, hipStream_t st, const uint64_t *keys,
 
 bool exchanging(const nas_ctx *ctx) { return ctx->world > 1 && !ctx->virtual_shard; }
 
+// The pod arrays a scoring pass reads and writes: the context's own, or the
+// gathered scratch view of a rescore (k_rescore.hip) with its own row stride.
+struct PodView {
+    const void *WA;
+    const int32_t *req;
+    int Pp;  // row stride of req / mask / partial lists
+    uint64_t *key, *bound;
+};
+
+PodView main_view(nas_ctx *ctx) {
+    return {ctx->WA.p, ctx->req.as<int32_t>(), ctx->Pp, ctx->cand_key.as<uint64_t>(),
+            ctx->cand_bound.as<uint64_t>()};
+}
+
 // scoring for pods [p_lo, p_hi) on stream st against capacity `cap`:
 // fit -> cost/top-k -> merge (-> exchange over the stream's communicator)
 int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nullptr,
-                const int32_t *cap = nullptr) {
+                const int32_t *cap = nullptr, const PodView *view = nullptr) {
     if (!st) st = ctx->stream;
     if (!cap) cap = ctx->cap.as<int32_t>();
+    const PodView v = view ? *view : main_view(ctx);
     const int sidx = st == ctx->stream2 ? 1 : 0;
     const int pr0 = p_lo / nas::COST_BN * nas::COST_BN;
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
     const int np = pr1 - pr0;
     auto *mask = ctx->mask.as<uint64_t>();
     hipEvent_t e0 = tm.mark(st);
-    HIPCK(nas::launch_fit(st, cap, ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
-                          ctx->req.as<int32_t>(), ctx->P, ctx->Pp, p_lo, p_hi - p_lo, mask));
+    HIPCK(nas::launch_fit(st, cap, ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp, v.req, p_hi, v.Pp, p_lo,
+                          p_hi - p_lo, mask));
     hipEvent_t e1 = tm.mark(st);
-    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, ctx->Pp,
-                                pr0, np, mask, ctx->partial.as<uint64_t>(),
-                                ctx->pbound.as<uint64_t>(), ctx->Nloc0));
+    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, v.WA, ctx->Mp, ctx->Kp, v.Pp, pr0, np,
+                                mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
+                                ctx->Nloc0));
     hipEvent_t e2 = tm.mark(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
-                            (int64_t)ctx->Pp * KC, ctx->Pp, 0, p_lo, p_hi - p_lo,
-                            ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>()));
+                            (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, v.key, v.bound));
     if (exchanging(ctx)) {
         // exchange the per-shard lists of pods [pr0, pr1) and merge across ranks
         auto *gk = ctx->gather[sidx].as<uint64_t>();
         auto *gb = ctx->gbound[sidx].as<uint64_t>();
-        OK(exchange(ctx, sidx ? ctx->comm2 : ctx->comm, st,
-                    ctx->cand_key.as<uint64_t>() + (size_t)pr0 * KC,
-                    ctx->cand_bound.as<uint64_t>() + pr0, (size_t)np, gk, gb));
+        OK(exchange(ctx, sidx ? ctx->comm2 : ctx->comm, st, v.key + (size_t)pr0 * KC, v.bound + pr0,
+                    (size_t)np, gk, gb));
         HIPCK(nas::launch_merge(st, gk, gb, ctx->world, (int64_t)np * KC, np, pr0, p_lo,
-                                p_hi - p_lo, ctx->cand_key.as<uint64_t>(),
-                                ctx->cand_bound.as<uint64_t>()));
+                                p_hi - p_lo, v.key, v.bound));
     }
     hipEvent_t e3 = tm.mark(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
     tm.span(T_MERGE, e2, e3);
     ctx->timings.cost_launches += 1;
+    return NAS_OK;
+}
+
+// Gathered rescore after the commit halted at pod `stop` (k_rescore.hip):
+// every pending pod whose list is dry against the capacity now (up to
+// GATHER_PODS of them, in pod order, `stop` first) is rescored through a
+// scratch view and its list written back.  Returns the number rescored.
+int rescore_gathered(nas_ctx *ctx, Timer &tm, int stop, int *n_out) {
+    hipStream_t st = ctx->stream;
+    const int P = ctx->P, R = std::min(GATHER_PODS, ctx->Pp);
+    const size_t row = (size_t)ctx->Kp * esz(ctx->dtype);
+    OK(nas::ensure(ctx, ctx->g_words, (size_t)nas::stale_words(ctx->Pp) * 8));
+    OK(nas::ensure(ctx, ctx->g_idx, (size_t)R * 4 + 64));
+    OK(nas::ensure(ctx, ctx->g_WA, (size_t)R * row));
+    OK(nas::ensure(ctx, ctx->g_req, (size_t)3 * R * 4));
+    OK(nas::ensure(ctx, ctx->g_key, (size_t)R * KC * 8));
+    OK(nas::ensure(ctx, ctx->g_bound, (size_t)R * 8));
+    int32_t *idx = ctx->g_idx.as<int32_t>(), *count = idx + R;
+    HIPCK(nas::launch_stale_scan(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                                 ctx->req.as<int32_t>(), ctx->Pp, ctx->cap.as<int32_t>(), ctx->N,
+                                 stop, P, ctx->g_words.as<uint64_t>(), R, idx, count));
+    int32_t *hs = ctx->host_status.as<int32_t>();
+    HIPCK(hipMemcpyAsync(hs + 3, count, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    const int n = hs[3];
+    if (n <= 0 || n > R) return nas::fail(ctx, NAS_ERR_HIP, "commit halted without a dry pod");
+    const int Rv = (int)nas::round_up(n, nas::COST_BN);
+    HIPCK(nas::launch_gather_pods(st, idx, count, ctx->WA.p, row, ctx->req.as<int32_t>(), ctx->Pp,
+                                  Rv, ctx->g_WA.p, ctx->g_req.as<int32_t>()));
+    const PodView v{ctx->g_WA.p, ctx->g_req.as<int32_t>(), Rv, ctx->g_key.as<uint64_t>(),
+                    ctx->g_bound.as<uint64_t>()};
+    OK(score_range(ctx, tm, 0, n, st, nullptr, &v));
+    HIPCK(nas::launch_scatter_lists(st, idx, count, Rv, ctx->g_key.as<uint64_t>(),
+                                    ctx->g_bound.as<uint64_t>(), ctx->cand_key.as<uint64_t>(),
+                                    ctx->cand_bound.as<uint64_t>()));
+    *n_out = n;
     return NAS_OK;
 }
 
@@ -258,7 +307,7 @@ int no_batch(nas_ctx *ctx, const char *what) {
 // ranks issue the same collectives).  Every pod of [s, hi) belongs to chunks
 // whose scoring the commit stream has already waited for: no other stream
 // touches their masks, partial lists or candidate lists.
-int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi) {
+int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi, int32_t *pub = nullptr) {
     int32_t *halt = ctx->status.as<int32_t>();
     const nas::Dyn dyn{halt, RESCORE_PODS, hi};
     const int B = ctx->B;  // batched: every cluster with a stop gets its own window
@@ -290,7 +339,7 @@ int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi) {
     HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), ctx->Pp, -1, hi, ctx->cap.as<int32_t>(),
                              ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
-                             halt, B));
+                             halt, B, pub));
     return NAS_OK;
 }
 
@@ -508,7 +557,8 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->gather[0], &ctx->gbound[0], &ctx->gather[1], &ctx->gbound[1],
                       &ctx->resc_key, &ctx->resc_bound, &ctx->gather_r, &ctx->gbound_r,
                       &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
-                      &ctx->status, &ctx->scratch};
+                      &ctx->g_words, &ctx->g_idx, &ctx->g_WA, &ctx->g_req, &ctx->g_key,
+                      &ctx->g_bound, &ctx->status, &ctx->scratch};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
@@ -843,11 +893,13 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // stream has left it so far: every value read is >= the capacity at the
     // chunk's pods' own (later) turn, so every node that will fit them is
     // scored (the lists stay exact) and the lists are far fresher than a
-    // snapshot at entry -- fewer pods exhaust them.  Only the LDS commit
-    // publishes final values alone; the L2 commit's speculative reservations
-    // could dip below them, so it scores against a snapshot at entry.
+    // snapshot at entry -- fewer pods exhaust them.  The LDS commit publishes
+    // final values only; the L2 commit's speculative reservations could dip
+    // below them, so it also maintains a published copy (cap_snap, start
+    // minus committed pods) that scoring reads instead.
     const bool live_cap = nas::commit_in_lds(N);
     const int32_t *score_cap = live_cap ? ctx->cap.as<int32_t>() : ctx->cap_snap.as<int32_t>();
+    int32_t *pub = live_cap ? nullptr : ctx->cap_snap.as<int32_t>();
     if (!live_cap)
         HIPCK(hipMemcpyAsync(ctx->cap_snap.p, ctx->cap.p, (size_t)3 * N * 4, hipMemcpyDeviceToDevice, st));
     HIPCK(hipMemsetAsync(halt, 0xff, 4, st));  // halt = -1
@@ -865,8 +917,9 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         hipEvent_t c0 = tm.mark(sc);
         HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
-                                 ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt));
-        for (int r = 0, n = rescore_slots(hi == P); r < n; ++r) OK(rescore_slot(ctx, sc, hi));
+                                 ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
+                                 1, pub));
+        for (int r = 0, n = rescore_slots(hi == P); r < n; ++r) OK(rescore_slot(ctx, sc, hi, pub));
         tm.span(T_COMMIT, c0, tm.mark(sc));
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
@@ -877,13 +930,15 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     const int dev_rounds = hs[1];
     int rounds = 0;
     while (hs[0] >= 0) {
-        // pod `stop` exhausted its candidates: rescore a window against the
-        // current capacity (lists computed now stay valid for later pods),
-        // then walk on from it
+        // pod `stop` exhausted its candidates: rescore it and every later pod
+        // whose list is dry too against the current capacity (lists computed
+        // now stay valid for later turns), then walk on from it
         const int stop = hs[0];
         if (stop >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
         if (++rounds > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
-        OK(score_range(ctx, tm, stop, std::min(P, stop + RESCORE_PODS)));
+        int n_dry = 0;
+        OK(rescore_gathered(ctx, tm, stop, &n_dry));
+        ctx->timings.rescored_pods += n_dry;
         HIPCK(hipMemsetAsync(halt, 0xff, 4, st));
         hipEvent_t c0 = tm.mark(st);
         HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),

@@ -76,7 +76,7 @@ struct nas_ctx {
     nas::DevBuf Lt;          // [Mp][Kp] elements: Lt[i][m] = L[m][Nloc0 + i]
     nas::DevBuf WA;          // [Pp][Kp] elements
     nas::DevBuf cap0, cap;   // [3][N] int32 (initial, working)
-    nas::DevBuf cap_snap;    // [3][N] working capacity at the start of nas_place (L2 commit)
+    nas::DevBuf cap_snap;    // [3][N] published capacity: start minus committed pods (L2 commit)
     nas::DevBuf req;         // [3][Pp] int32
     nas::DevBuf mask;        // [ceil(Mp/64)][Pp] uint64, local nodes
     nas::DevBuf partial;     // [Mp/BM][Pp][KC] uint64 keys per node tile
@@ -88,6 +88,8 @@ struct nas_ctx {
     nas::DevBuf resc_key, resc_bound;      // rescore slot staging [win][KC] / [win] (multi-GPU)
     nas::DevBuf gather_r, gbound_r;        // rescore slot exchange [world][win][KC] / [world][win]
     nas::DevBuf out_node, out_cost_f, out_cost_i;  // [Pp]
+    nas::DevBuf g_words, g_idx;            // gathered rescore: dry-pod ballots, indices + count
+    nas::DevBuf g_WA, g_req, g_key, g_bound;  // gathered rescore view [R][Kp] / [3][R] / lists
     nas::DevBuf status;      // small device scratch for commit control
     nas::DevBuf host_status; // pinned
     nas::DevBuf scratch;
@@ -147,7 +149,20 @@ hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bo
 bool commit_in_lds(int N);
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
-                         int32_t *out_node, int32_t *out_cost_i, int32_t *halt, int batch = 1);
+                         int32_t *out_node, int32_t *out_cost_i, int32_t *halt, int batch = 1,
+                         int32_t *pub = nullptr);
+
+// gathered rescore (k_rescore.hip)
+int stale_words(int P);
+hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t *bound,
+                             const int32_t *req, int Pp, const int32_t *cap, int N, int p0, int P,
+                             uint64_t *words, int R, int32_t *idx, int32_t *count);
+hipError_t launch_gather_pods(hipStream_t st, const int32_t *idx, const int32_t *count,
+                              const void *WA, size_t row_bytes, const int32_t *req, int Pp, int Rv,
+                              void *WA_v, int32_t *req_v);
+hipError_t launch_scatter_lists(hipStream_t st, const int32_t *idx, const int32_t *count, int Rv,
+                                const uint64_t *key_v, const uint64_t *bound_v, uint64_t *key,
+                                uint64_t *bound);
 
 hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
                               int nloc, int Mp, int Kp, void *Lt);

@@ -58,3 +58,20 @@ def test_batch_rejects_shards():
         e.set_batch(2)
         with pytest.raises(Exception):
             e.set_shard(0, 2)
+
+
+def test_c2_workload_equals_oracle():
+    """BASELINE config C2 at full size (1k nodes x 10k pods, CSR traffic)."""
+    from kubernetesnetawarescheduler_amd import workloads
+    c = workloads.c2_cluster(0x4E4153, 1000, 10000)
+    with Engine(0) as e:
+        e.upload_latency(c["L"], "i8")
+        e.upload_capacity(c["free"])
+        e.upload_pods(c["req"])
+        e.upload_traffic_csr(c["row_ptr"], c["peer_node"], c["weight"], "i8", 1000)
+        node, _, score = e.place()
+        cap = e.get_capacity()
+    WA = workloads.csr_to_dense(c["row_ptr"], c["peer_node"], c["weight"], 1000)
+    want, wcost, wfree = oracle.place(WA, c["L"], c["req"], c["free"], "i8")
+    assert node.tolist() == want.tolist() and score.tolist() == wcost.tolist()
+    assert (cap == wfree).all()

@@ -1,0 +1,47 @@
+"""C2 generator (kubernetesnetawarescheduler_amd/workloads.py): the
+clusterloader2 request distribution (Cpu 0.000213-0.5376
+cores, Mem 7,643,136-311,037,952 B over 408 rows), the CSR shape, and the
+oracle on the densified traffic."""
+import numpy as np
+
+import oracle
+from kubernetesnetawarescheduler_amd import workloads
+
+
+def test_clusterloader2_rows():
+    cpu, mem = workloads.clusterloader2_requests()
+    assert len(cpu) == len(mem) == 408
+    assert cpu.min() == 1 and cpu.max() == 538  # ceil(0.000213e3), ceil(0.5376e3)
+    assert mem.min() == 7643136 // 1024 and mem.max() == -(-311037952 // 1024)
+
+
+def test_c2_shape_and_determinism():
+    a = workloads.c2_cluster(7, N=200, P=1000)
+    b = workloads.c2_cluster(7, N=200, P=1000)
+    for k in a:
+        assert (a[k] == b[k]).all(), k
+    L = a["L"]
+    assert (L == L.T).all() and (np.diag(L) == 0).all()
+    off = L[~np.eye(200, dtype=bool)]
+    assert off.min() >= 12 and off.max() <= 125
+    rp = a["row_ptr"]
+    assert rp[0] == 0 and rp[-1] == len(a["peer_node"]) and (np.diff(rp) <= 8).all()
+    assert ((a["peer_node"] >= 0) & (a["peer_node"] < 200)).all()
+    assert (a["weight"] >= 1).all() and (a["weight"] <= 100).all()
+    assert (a["req"][:, 2] == 1).all()
+
+
+def test_csr_to_dense_saturates():
+    rp = np.array([0, 3], np.int32)
+    pn = np.array([1, 1, 2], np.int32)
+    w = np.array([100, 100, 5], np.int8)
+    WA = workloads.csr_to_dense(rp, pn, w, 4)
+    assert WA.tolist() == [[0, 127, 5, 0]]
+
+
+def test_c2_oracle_places_everything():
+    c = workloads.c2_cluster(1, N=100, P=1000)
+    WA = workloads.csr_to_dense(c["row_ptr"], c["peer_node"], c["weight"], 100)
+    node, _, free = oracle.place(WA, c["L"], c["req"], c["free"], "i8")
+    assert (node >= 0).all() and (free >= 0).all()
+    assert np.bincount(node, minlength=100).max() <= 110
