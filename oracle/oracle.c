@@ -197,18 +197,25 @@ int or_vote_batch(int n, int n_snapshots, const double *cpu, const double *mem,
                   const int64_t *rx, const int64_t *tx, const double *bw, const int64_t *disk,
                   const int32_t *order1, const int32_t *order2, int n_orders,
                   const int32_t *pod_snapshot, int P, int32_t *best_out, int32_t *winners_out) {
+    int err = 0;
+    /* pods are independent (one Schedule call each); OMP_NUM_THREADS=1 is the
+     * reference's single goroutine */
+#pragma omp parallel for schedule(dynamic, 16) reduction(| : err)
     for (int p = 0; p < P; ++p) {
         int s = pod_snapshot ? pod_snapshot[p] : p;
-        if (s < 0 || s >= n_snapshots) return -1;
+        if (s < 0 || s >= n_snapshots) {
+            err |= 1;
+            continue;
+        }
         int o = n_orders == 1 ? 0 : s;
         size_t b = (size_t)s * n;
         int rc = or_vote_literal(n, cpu + b, mem + b, rx + b, tx + b, bw + b, disk + b,
                                  order1 + (size_t)o * n, order2 + (size_t)o * (n + 1),
                                  best_out + p, winners_out ? winners_out + (size_t)6 * p : NULL,
                                  NULL);
-        if (rc) return rc;
+        if (rc) err |= 1;
     }
-    return 0;
+    return err ? -1 : 0;
 }
 
 /* ------------------------------------------------------------------------ */
