@@ -32,11 +32,11 @@ PEAK_BF16_TFLOPS = 2516.6  # dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # HBM3E spec (MI355X_MICROARCH.md)
 SEED = 0x4E4153
 # HBM-side bytes per launch from rocprofv3 PMC passes (tools/prof_bench.sh ->
-# profiles/r01_prof_summary.json): FETCH_SIZE x 2 (gfx950 correction,
+# profiles/r01_final_prof_summary.json): FETCH_SIZE x 2 (gfx950 correction,
 # MI355X_MICROARCH.md) + WRITE_SIZE, for the default workload on one GPU only;
 # any other (kernel, dtype, nodes, pods, world) reports null.
-PMC_TRAFFIC = {("k_cost_topk", "i8", 10000, 100000, 1): 16785070208.0,
-               ("k_vote", "i8", 10000, 100000, 1): 48088185536.0}
+PMC_TRAFFIC = {("k_cost_topk", "i8", 10000, 100000, 1): 16804332288.0,
+               ("k_vote", "i8", 10000, 100000, 1): 48087768832.0}
 
 
 def parse():
