@@ -14,9 +14,9 @@
 // Parallel form: one 1024-thread workgroup, one pod per thread, a window of
 // 1024 consecutive pods per round.
 //   1. Every pending pod picks its first fitting usable candidate against the
-//      capacity at the start of the round and RESERVES it with per-resource
-//      compare-and-swap loops that never take a resource below zero (so no
-//      overflow, whatever the request sizes).
+//      capacity at the start of the round and RESERVES it per resource (a
+//      fetch-and-subtract undone on failure, or for huge requests a
+//      compare-and-swap loop that never goes below zero; see reserve()).
 //   2. A pod is BAD if a reservation failed or it needs a rescore; s = the
 //      lowest bad pod (LDS atomicMin).
 //   3. Every pod below s is exactly what the sequential walk does: for the
@@ -47,11 +47,27 @@ constexpr int LDS_DYN_MAX = 160 * 1024 - 512;  // leaves room for the static LDS
 constexpr int LDS_CAP_MAX_NODES = LDS_DYN_MAX / 12;
 constexpr int NO_POD = 0x7fffffff;
 
-// reserve r from *c iff *c >= r, never going below zero; returns success
+// Requests up to this size reserve with one fetch-and-subtract (undone on
+// failure) instead of a compare-and-swap loop: a herd of m pods picking one
+// node then costs m atomics, not ~m^2 retries.  The dips of failed
+// subtractions are transient and can only make a concurrent reservation fail
+// spuriously (one more round), never succeed wrongly; THREADS of them stay
+// above INT_MIN (1024 * 2^21 = 2^31).  Larger requests keep the CAS loop,
+// which never takes a resource below zero.
+constexpr int FETCH_SUB_MAX = 1 << 21;
+
+// reserve r from *c iff *c >= r; returns success
 template <bool LDS_CAP>
 __device__ __forceinline__ bool reserve(int *c, int r) {
     if (r == 0) return true;
     int old = LDS_CAP ? *c : __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old < r) return false;
+    if (r <= FETCH_SUB_MAX) {
+        const int prev = atomicSub(c, r);
+        if (prev >= r) return true;
+        atomicAdd(c, r);
+        return false;
+    }
     while (old >= r) {
         const int prev = atomicCAS(c, old, old - r);
         if (prev == old) return true;

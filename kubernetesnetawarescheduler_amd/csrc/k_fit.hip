@@ -30,12 +30,14 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 __global__ void __launch_bounds__(FIT_THREADS)
 k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
       const int *__restrict__ req, int Pp, int p0, int p_end, unsigned long long *__restrict__ mask,
-      const int *__restrict__ dyn_start, int dyn_win) {
+      const int *__restrict__ dyn_start, int dyn_win, const int *__restrict__ dyn_hi_ptr) {
     if (dyn_start) {  // window [*dyn_start, +dyn_win) read from device memory (rescore slots)
         const int s = dyn_start[blockIdx.z * STATUS_INTS];
         if (s < 0) return;
         p0 = s;
+        if (dyn_hi_ptr) p_end = dyn_hi_ptr[blockIdx.z * STATUS_INTS];
         p_end = min(p_end, s + dyn_win);
+        if (p0 + (int)blockIdx.x * FIT_THREADS >= p_end) return;  // whole block
     }
     const int cb = blockIdx.z;  // cluster of a batched launch
     cap += (size_t)cb * 3 * N;
@@ -96,7 +98,8 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
     k_fit<<<grid, FIT_THREADS, 0, st>>>(cap, N, n0, nloc, n_chunks, req, Pp, p0,
                                         dyn ? dyn->hi : p0 + np,
                                         reinterpret_cast<unsigned long long *>(mask),
-                                        dyn ? dyn->start : nullptr, dyn ? dyn->win : 0);
+                                        dyn ? dyn->start : nullptr, dyn ? dyn->win : 0,
+                                        dyn ? dyn->hi_ptr : nullptr);
     return hipGetLastError();
 }
 

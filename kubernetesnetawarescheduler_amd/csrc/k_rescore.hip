@@ -25,29 +25,37 @@ namespace {
 
 constexpr int STALE_THREADS = 256;
 constexpr int COMPACT_THREADS = 1024;
+// a pod is flagged when fewer than this many of its usable candidates still
+// fit: the dry ones (0) and those one commit away from running dry, whose
+// lists a herd of neighbours is about to drain
+#ifndef STALE_MIN_FIT
+#define STALE_MIN_FIT 2
+#endif
 
 __global__ void __launch_bounds__(STALE_THREADS)
 k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *__restrict__ req,
-        int Pp, const int *__restrict__ cap, int N, int p0, int P, u64 *__restrict__ words) {
+        int Pp, const int *__restrict__ cap, int N, int p0, int P, u64 *__restrict__ words,
+        const int *__restrict__ p0_dev) {
     const int t = blockIdx.x * STALE_THREADS + threadIdx.x;
     const int p = p0 + t;
+    // device-side slot: pods from the halt word on (none when it is < 0)
+    const int first = p0_dev ? *p0_dev : p0;
     bool dry = false;
-    if (p < P) {
+    if (p < P && first >= 0 && p >= first) {
         const u64 b = bound[p];
         if (b != KEY_INVALID) {
             u64 k[KC];
             load8(key + (size_t)p * KC, k);
             const int r0 = req[p], r1 = req[Pp + p], r2 = req[2 * Pp + p];
-            dry = true;
+            int fits = 0;
 #pragma unroll
             for (int j = 0; j < KC; ++j) {
                 if (k[j] == KEY_INVALID || k[j] > b) break;
                 const int n = (int)(unsigned)k[j];
-                if (r0 <= cap[n] && r1 <= cap[N + n] && r2 <= cap[2 * N + n]) {
-                    dry = false;
-                    break;
-                }
+                fits += (r0 <= cap[n] && r1 <= cap[N + n] && r2 <= cap[2 * N + n]) ? 1 : 0;
+                if (fits >= STALE_MIN_FIT) break;
             }
+            dry = fits < STALE_MIN_FIT;
         }
     }
     const u64 m = __ballot(dry);
@@ -56,7 +64,7 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
 
 __global__ void __launch_bounds__(COMPACT_THREADS)
 k_compact(const u64 *__restrict__ words, int n_words, int p0, int R, int *__restrict__ idx,
-          int *__restrict__ count) {
+          int *__restrict__ ctl) {
     __shared__ int part[COMPACT_THREADS];
     const int tid = threadIdx.x;
     const int per = (n_words + COMPACT_THREADS - 1) / COMPACT_THREADS;
@@ -73,7 +81,12 @@ k_compact(const u64 *__restrict__ words, int n_words, int p0, int R, int *__rest
         __syncthreads();
     }
     int off = part[tid] - c;
-    if (tid == COMPACT_THREADS - 1) *count = min(part[tid], R);
+    if (tid == COMPACT_THREADS - 1) {
+        const int n = min(part[tid], R);
+        ctl[0] = n > 0 ? 0 : -1;  // the view's window start, read like a halt word
+        ctl[1] = n;
+        ctl[2] += n;              // running total, reported in nas_timings
+    }
     for (int w = w0; w < w1 && off < R; ++w) {
         u64 m = words[w];
         while (m && off < R) {
@@ -85,18 +98,18 @@ k_compact(const u64 *__restrict__ words, int n_words, int p0, int R, int *__rest
 }
 
 // one workgroup per view row: row i < count copies pod idx[i]'s traffic row
-// and requests, rows past count are zero (scored, never scattered)
+// and requests
 __global__ void __launch_bounds__(256)
 k_gather_pods(const int *__restrict__ idx, const int *__restrict__ count, const uint4 *__restrict__ WA,
               int row_vec, const int *__restrict__ req, int Pp, int Rv, uint4 *__restrict__ WA_v,
               int *__restrict__ req_v) {
     const int i = blockIdx.x;
-    const bool live = i < *count;
-    const int p = live ? idx[i] : 0;
+    if (i >= *count) return;  // rows past count are scored as garbage and never scattered
+    const int p = idx[i];
     const uint4 *src = WA + (size_t)p * row_vec;
     uint4 *dst = WA_v + (size_t)i * row_vec;
-    for (int v = threadIdx.x; v < row_vec; v += 256) dst[v] = live ? src[v] : make_uint4(0, 0, 0, 0);
-    if (threadIdx.x < 3) req_v[threadIdx.x * Rv + i] = live ? req[threadIdx.x * Pp + p] : 0;
+    for (int v = threadIdx.x; v < row_vec; v += 256) dst[v] = src[v];
+    if (threadIdx.x < 3) req_v[threadIdx.x * Rv + i] = req[threadIdx.x * Pp + p];
 }
 
 __global__ void k_scatter_lists(const int *__restrict__ idx, const int *__restrict__ count,
@@ -116,15 +129,17 @@ int stale_words(int P) { return (P + STALE_THREADS - 1) / STALE_THREADS * (STALE
 
 hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t *bound,
                              const int32_t *req, int Pp, const int32_t *cap, int N, int p0, int P,
-                             uint64_t *words, int R, int32_t *idx, int32_t *count) {
+                             uint64_t *words, int R, int32_t *idx, int32_t *ctl,
+                             const int32_t *p0_dev) {
+    if (p0 < 0) p0 = 0;  // device-side start: scan every pod, k_stale skips those before it
     const int n = P - p0;
     if (n <= 0) return hipErrorInvalidValue;
     const int blocks = (n + STALE_THREADS - 1) / STALE_THREADS;
     auto *w = reinterpret_cast<u64 *>(words);
     k_stale<<<blocks, STALE_THREADS, 0, st>>>(reinterpret_cast<const u64 *>(key),
                                               reinterpret_cast<const u64 *>(bound), req, Pp, cap, N,
-                                              p0, P, w);
-    k_compact<<<1, COMPACT_THREADS, 0, st>>>(w, blocks * (STALE_THREADS / 64), p0, R, idx, count);
+                                              p0, P, w, p0_dev);
+    k_compact<<<1, COMPACT_THREADS, 0, st>>>(w, blocks * (STALE_THREADS / 64), p0, R, idx, ctl);
     return hipGetLastError();
 }
 

@@ -62,7 +62,8 @@ int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes) {
 namespace {
 
 constexpr int RESCORE_PODS = 1024;  // pods per device-side rescore slot (multiple of COST_BN)
-constexpr int GATHER_PODS = 4096;   // dry pods rescored per host-side stop (rescore_gathered)
+constexpr int GATHER_PODS = 4096;   // dry pods rescored per gathered slot (gathered_slot)
+constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
 // Device-side rescore slots enqueued behind a chunk's commit.  An idle slot
 // still costs its launches a wait for free CUs while scoring fills the chip,
 // and scoring against the live capacity makes stops rare, so by default only
@@ -256,39 +257,69 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     return NAS_OK;
 }
 
-// Gathered rescore after the commit halted at pod `stop` (k_rescore.hip):
-// every pending pod whose list is dry against the capacity now (up to
-// GATHER_PODS of them, in pod order, `stop` first) is rescored through a
-// scratch view and its list written back.  Returns the number rescored.
-int rescore_gathered(nas_ctx *ctx, Timer &tm, int stop, int *n_out) {
-    hipStream_t st = ctx->stream;
-    const int P = ctx->P, R = std::min(GATHER_PODS, ctx->Pp);
+// Gathered rescore slot, all on the device (k_rescore.hip): if the commit walk
+// has halted (halt word >= 0), every pending pod in [halt, hi) whose list is
+// dry against the capacity now -- up to GATHER_PODS of them, in pod order, the
+// halted pod first -- is copied into a scratch view, scored there by the
+// ordinary fit / cost / merge kernels (+ the exchange across ranks), its list
+// written back, and the walk resumed from the halt.  Nothing halted: every
+// kernel exits at once (the exchange still runs, so all ranks issue the same
+// collectives).  Slots need no host round trip, so a crowded cluster's many
+// stops cost launches, not synchronisations.
+int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t *pub, int hi) {
+    const int R = std::min(GATHER_PODS, ctx->Pp);
     const size_t row = (size_t)ctx->Kp * esz(ctx->dtype);
     OK(nas::ensure(ctx, ctx->g_words, (size_t)nas::stale_words(ctx->Pp) * 8));
-    OK(nas::ensure(ctx, ctx->g_idx, (size_t)R * 4 + 64));
+    OK(nas::ensure(ctx, ctx->g_idx, (size_t)R * 4));
     OK(nas::ensure(ctx, ctx->g_WA, (size_t)R * row));
     OK(nas::ensure(ctx, ctx->g_req, (size_t)3 * R * 4));
     OK(nas::ensure(ctx, ctx->g_key, (size_t)R * KC * 8));
     OK(nas::ensure(ctx, ctx->g_bound, (size_t)R * 8));
-    int32_t *idx = ctx->g_idx.as<int32_t>(), *count = idx + R;
+    int32_t *halt = ctx->status.as<int32_t>();
+    int32_t *ctl = halt + nas::STATUS_INTS;  // {view start, count, rescored total}
+    int32_t *idx = ctx->g_idx.as<int32_t>();
+    auto *gk = ctx->g_key.as<uint64_t>();
+    auto *gb = ctx->g_bound.as<uint64_t>();
+    hipEvent_t e0 = tm.mark(st);
     HIPCK(nas::launch_stale_scan(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, ctx->cap.as<int32_t>(), ctx->N,
-                                 stop, P, ctx->g_words.as<uint64_t>(), R, idx, count));
-    int32_t *hs = ctx->host_status.as<int32_t>();
-    HIPCK(hipMemcpyAsync(hs + 3, count, 4, hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
-    const int n = hs[3];
-    if (n <= 0 || n > R) return nas::fail(ctx, NAS_ERR_HIP, "commit halted without a dry pod");
-    const int Rv = (int)nas::round_up(n, nas::COST_BN);
-    HIPCK(nas::launch_gather_pods(st, idx, count, ctx->WA.p, row, ctx->req.as<int32_t>(), ctx->Pp,
-                                  Rv, ctx->g_WA.p, ctx->g_req.as<int32_t>()));
-    const PodView v{ctx->g_WA.p, ctx->g_req.as<int32_t>(), Rv, ctx->g_key.as<uint64_t>(),
-                    ctx->g_bound.as<uint64_t>()};
-    OK(score_range(ctx, tm, 0, n, st, nullptr, &v));
-    HIPCK(nas::launch_scatter_lists(st, idx, count, Rv, ctx->g_key.as<uint64_t>(),
-                                    ctx->g_bound.as<uint64_t>(), ctx->cand_key.as<uint64_t>(),
+                                 -1, hi, ctx->g_words.as<uint64_t>(), R, idx, ctl, halt));
+    HIPCK(nas::launch_gather_pods(st, idx, ctl + 1, ctx->WA.p, row, ctx->req.as<int32_t>(),
+                                  ctx->Pp, R, ctx->g_WA.p, ctx->g_req.as<int32_t>()));
+    nas::Dyn dyn{ctl, R, 0, ctl + 1};
+    auto *mask = ctx->mask.as<uint64_t>();
+    hipEvent_t e1 = tm.mark(st);
+    HIPCK(nas::launch_fit(st, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
+                          ctx->g_req.as<int32_t>(), R, R, 0, R, mask, &dyn));
+    hipEvent_t e2 = tm.mark(st);
+    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->g_WA.p, ctx->Mp, ctx->Kp, R, 0, 0,
+                                mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
+                                ctx->Nloc0, &dyn));
+    hipEvent_t e3 = tm.mark(st);
+    const int n_lists = ctx->Mp / nas::COST_BM;
+    HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
+                            (int64_t)R * KC, R, 0, 0, 0, gk, gb, 0, &dyn, 0));
+    if (exchanging(ctx)) {
+        OK(nas::ensure(ctx, ctx->g_gk, (size_t)ctx->world * R * KC * 8));
+        OK(nas::ensure(ctx, ctx->g_gb, (size_t)ctx->world * R * 8));
+        auto *xk = ctx->g_gk.as<uint64_t>();
+        auto *xb = ctx->g_gb.as<uint64_t>();
+        OK(exchange(ctx, cm, st, gk, gb, (size_t)R, xk, xb));
+        HIPCK(nas::launch_merge(st, xk, xb, ctx->world, (int64_t)R * KC, R, 0, 0, 0, gk, gb, 0,
+                                &dyn, 0));
+    }
+    HIPCK(nas::launch_scatter_lists(st, idx, ctl + 1, R, gk, gb, ctx->cand_key.as<uint64_t>(),
                                     ctx->cand_bound.as<uint64_t>()));
-    *n_out = n;
+    hipEvent_t e4 = tm.mark(st);
+    HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                             ctx->req.as<int32_t>(), ctx->Pp, -1, hi, ctx->cap.as<int32_t>(),
+                             ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
+                             halt, 1, pub));
+    tm.span(T_FIT, e1, e2);
+    tm.span(T_COST, e2, e3);
+    tm.span(T_MERGE, e3, e4);
+    tm.span(T_COMMIT, e0, e1);
+    tm.span(T_COMMIT, e4, tm.mark(st));
     return NAS_OK;
 }
 
@@ -558,7 +589,7 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->resc_key, &ctx->resc_bound, &ctx->gather_r, &ctx->gbound_r,
                       &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
                       &ctx->g_words, &ctx->g_idx, &ctx->g_WA, &ctx->g_req, &ctx->g_key,
-                      &ctx->g_bound, &ctx->status, &ctx->scratch};
+                      &ctx->g_bound, &ctx->g_gk, &ctx->g_gb, &ctx->status, &ctx->scratch};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
@@ -904,6 +935,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         HIPCK(hipMemcpyAsync(ctx->cap_snap.p, ctx->cap.p, (size_t)3 * N * 4, hipMemcpyDeviceToDevice, st));
     HIPCK(hipMemsetAsync(halt, 0xff, 4, st));  // halt = -1
     HIPCK(hipMemsetAsync(halt + 1, 0, 8, st));  // device-side rescores, commit rounds
+    HIPCK(hipMemsetAsync(halt + nas::STATUS_INTS, 0, 16, st));  // gathered-slot control
     hipEvent_t ready = tm.mark(st);
     HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
     HIPCK(hipStreamWaitEvent(sc, ready, 0));
@@ -919,36 +951,28 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
                                  1, pub));
-        for (int r = 0, n = rescore_slots(hi == P); r < n; ++r) OK(rescore_slot(ctx, sc, hi, pub));
         tm.span(T_COMMIT, c0, tm.mark(sc));
+        for (int r = 0, n = rescore_slots(hi == P); r < n; ++r)
+            OK(gathered_slot(ctx, tm, sc, ctx->comm_c, pub, hi));
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
     HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
     int32_t *hs = ctx->host_status.as<int32_t>();
-    HIPCK(hipMemcpyAsync(hs, halt, 12, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hs, halt, 4, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    const int dev_rounds = hs[1];
-    int rounds = 0;
+    int checks = 0;
     while (hs[0] >= 0) {
-        // pod `stop` exhausted its candidates: rescore it and every later pod
-        // whose list is dry too against the current capacity (lists computed
-        // now stay valid for later turns), then walk on from it
-        const int stop = hs[0];
-        if (stop >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
-        if (++rounds > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
-        int n_dry = 0;
-        OK(rescore_gathered(ctx, tm, stop, &n_dry));
-        ctx->timings.rescored_pods += n_dry;
-        HIPCK(hipMemsetAsync(halt, 0xff, 4, st));
-        hipEvent_t c0 = tm.mark(st);
-        HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
-                                 ctx->req.as<int32_t>(), ctx->Pp, stop, P, ctx->cap.as<int32_t>(), N,
-                                 ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt));
-        tm.span(T_COMMIT, c0, tm.mark(st));
+        // still halted after the pipeline: more gathered slots, checked in batches
+        if (hs[0] >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
+        if (++checks > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
+        for (int r = 0; r < GATHER_SLOTS_PER_SYNC; ++r)
+            OK(gathered_slot(ctx, tm, st, ctx->comm, nullptr, P));
         HIPCK(hipMemcpyAsync(hs, halt, 4, hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
     }
-    HIPCK(hipMemcpyAsync(hs + 2, halt + 2, 4, hipMemcpyDeviceToHost, st));
+    // halt[1..2]: slot resumes, commit rounds; ctl[2]: pods rescored by slots
+    HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
     std::vector<uint32_t> raw;
     HIPCK(hipMemcpyAsync(node_out, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
     if (cost_out || int_score_out) {
@@ -972,7 +996,8 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     ctx->timings.merge_ms = tm.total(T_MERGE);
     ctx->timings.commit_ms = tm.total(T_COMMIT);
     ctx->timings.total_ms = tm.total(T_TOTAL);
-    ctx->timings.rescore_rounds = rounds + dev_rounds;
+    ctx->timings.rescore_rounds = hs[1];
+    ctx->timings.rescored_pods = hs[3];
     ctx->timings.unschedulable = unsched;
     ctx->timings.commit_rounds = hs[2];
     ctx->scored = true;

@@ -90,6 +90,7 @@ struct nas_ctx {
     nas::DevBuf out_node, out_cost_f, out_cost_i;  // [Pp]
     nas::DevBuf g_words, g_idx;            // gathered rescore: dry-pod ballots, indices + count
     nas::DevBuf g_WA, g_req, g_key, g_bound;  // gathered rescore view [R][Kp] / [3][R] / lists
+    nas::DevBuf g_gk, g_gb;                // gathered rescore exchange [world][R][KC] / [world][R]
     nas::DevBuf status;      // small device scratch for commit control
     nas::DevBuf host_status; // pinned
     nas::DevBuf scratch;
@@ -127,6 +128,7 @@ struct Dyn {
     const int32_t *start;
     int win;
     int hi;
+    const int32_t *hi_ptr = nullptr;  // when set, hi is read on the device (per cluster)
 };
 constexpr int MERGE_SRC_WINDOW = 1;  // k_merge source lists indexed from the window start
 constexpr int MERGE_DST_WINDOW = 2;  // k_merge destination indexed from the window start
@@ -154,9 +156,13 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
 
 // gathered rescore (k_rescore.hip)
 int stale_words(int P);
+// p0 < 0: the scan starts at the commit's halt word *p0_dev (nothing to do if
+// it is < 0); ctl receives {window start (0, or -1 when no pod is dry),
+// count, running total of rescored pods}
 hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t *bound,
                              const int32_t *req, int Pp, const int32_t *cap, int N, int p0, int P,
-                             uint64_t *words, int R, int32_t *idx, int32_t *count);
+                             uint64_t *words, int R, int32_t *idx, int32_t *ctl,
+                             const int32_t *p0_dev = nullptr);
 hipError_t launch_gather_pods(hipStream_t st, const int32_t *idx, const int32_t *count,
                               const void *WA, size_t row_bytes, const int32_t *req, int Pp, int Rv,
                               void *WA_v, int32_t *req_v);

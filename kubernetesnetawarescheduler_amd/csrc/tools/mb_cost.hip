@@ -59,7 +59,7 @@ int main(int argc, char **argv) {
         for (int v = 0; v < nv; ++v) {
             if (!strchr(vsel, 'a' + v)) continue;
             void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero,
-                            (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero};
+                            (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero, &nodyn};
             CK(hipEventRecord(a));
             CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(THREADS), args, vars[v].lds, 0));
             CK(hipEventRecord(b));
