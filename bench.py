@@ -52,9 +52,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the other BASELINE configs (C1/C2/C5 lines under 'configs')")
+                    help="skip the other BASELINE configs (C1/C2/C5/C4 lines under 'configs', "
+                         "one GPU only)")
     ap.add_argument("--c4", action="store_true",
-                    help="also run C4 (50k nodes x 500k pods) on this GPU count")
+                    help="run C4 (50k nodes x 500k pods, node-sharded) also when --gpus > 1")
     ap.add_argument("--only", choices=["place", "vote", "score"], default=None,
                     help="profile helper: run only one path")
     return ap.parse_args()
@@ -339,10 +340,10 @@ def config_c4(args, d, eng, N=50000, P=500000):
 
 
 def run_configs(args, d):
-    """The other BASELINE configs, each on a fresh context (rank 0, one GPU)."""
+    """The other BASELINE configs, each on a fresh context (one GPU)."""
     from kubernetesnetawarescheduler_amd import Engine
     out = {}
-    for name, fn in (("C1", config_c1), ("C2", config_c2), ("C5", config_c5)):
+    for name, fn in (("C1", config_c1), ("C2", config_c2), ("C5", config_c5), ("C4", config_c4)):
         with Engine(d.local) as e:
             out[name] = fn(args, d, e)
     return out
@@ -413,7 +414,7 @@ def main():
     eng.close()
     if d.world == 1 and not args.no_configs and args.only is None:
         out["configs"] = run_configs(args, d)
-    if args.c4:
+    if args.c4 and "C4" not in out.get("configs", {}):
         from kubernetesnetawarescheduler_amd import Engine
         with Engine(d.local) as e:
             out.setdefault("configs", {})["C4"] = config_c4(args, d, e)

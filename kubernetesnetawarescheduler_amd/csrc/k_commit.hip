@@ -76,6 +76,45 @@ __device__ __forceinline__ bool reserve(int *c, int r) {
     return false;
 }
 
+// A barrier inside the walk.  With the capacity in LDS every value the next
+// step reads is in LDS, so waiting for this wave's LDS operations is enough; a
+// full __syncthreads would also drain the next window's prefetch loads (and
+// the output stores) at every round.  The L2 form keeps the full fence: its
+// capacity updates are global atomics.
+template <bool LDS_CAP>
+__device__ __forceinline__ void round_barrier() {
+    if constexpr (LDS_CAP) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    } else {
+        __syncthreads();
+    }
+}
+
+// all three resources of a pick: with small requests the three
+// fetch-and-subtracts are in flight together (no load before them: a request
+// that plainly does not fit dips and undoes like any failed one)
+template <bool LDS_CAP>
+__device__ __forceinline__ void reserve3(int *c0, int *c1, int *c2, int r0, int r1, int r2,
+                                         bool &g0, bool &g1, bool &g2) {
+    if (r0 <= FETCH_SUB_MAX && r1 <= FETCH_SUB_MAX && r2 <= FETCH_SUB_MAX) {
+        const int p0 = r0 ? atomicSub(c0, r0) : 0;
+        const int p1 = r1 ? atomicSub(c1, r1) : 0;
+        const int p2 = r2 ? atomicSub(c2, r2) : 0;
+        g0 = p0 >= r0;
+        g1 = p1 >= r1;
+        g2 = p2 >= r2;
+        if (!g0) atomicAdd(c0, r0);
+        if (!g1) atomicAdd(c1, r1);
+        if (!g2) atomicAdd(c2, r2);
+        return;
+    }
+    g0 = reserve<LDS_CAP>(c0, r0);
+    g1 = reserve<LDS_CAP>(c1, r1);
+    g2 = reserve<LDS_CAP>(c2, r2);
+}
+
 template <bool LDS_CAP>
 __global__ void __launch_bounds__(THREADS)
 k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
@@ -109,8 +148,23 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     } else if (h >= 0) {
         return;
     }
-    if (LDS_CAP)
-        for (int i = tid; i < 3 * N; i += THREADS) capl[i] = cap_g[i];
+    if (LDS_CAP) {
+        // 8 loads in flight per thread: a plain copy loop waits out one global
+        // load latency per element (3N / 1024 of them, ~50 us at 10k nodes)
+        for (int i0 = tid; i0 < 3 * N; i0 += 8 * THREADS) {
+            int v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * THREADS;
+                v[u] = i < 3 * N ? cap_g[i] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * THREADS;
+                if (i < 3 * N) capl[i] = v[u];
+            }
+        }
+    }
     int *cap = LDS_CAP ? capl : cap_g;
     if (tid == 0) first_bad[0] = first_bad[1] = first_bad[2] = NO_POD;
 
@@ -186,17 +240,15 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             const bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
             // every pick must see the capacity at the START of the round: a
             // later pod's reservation must not push an earlier pod off a node
-            __syncthreads();
+            round_barrier<LDS_CAP>();
             bool g0 = false, g1 = false, g2 = false;
-            if (choice >= 0) {
-                g0 = reserve<LDS_CAP>(cap + choice, cur.r0);
-                g1 = reserve<LDS_CAP>(cap + N + choice, cur.r1);
-                g2 = reserve<LDS_CAP>(cap + 2 * N + choice, cur.r2);
-            }
+            if (choice >= 0)
+                reserve3<LDS_CAP>(cap + choice, cap + N + choice, cap + 2 * N + choice, cur.r0,
+                                  cur.r1, cur.r2, g0, g1, g2);
             const bool bad = rescore || (choice >= 0 && !(g0 && g1 && g2));
             int *fb = &first_bad[round % 3];
             if (bad) atomicMin(fb, i);
-            __syncthreads();
+            round_barrier<LDS_CAP>();
             // 2. the lowest bad pod
             const int s = *fb;
             ++round;
@@ -222,7 +274,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 done = true;
             }
             if (i == s) s_rescore = rescore;
-            __syncthreads();
+            round_barrier<LDS_CAP>();
             // a rescore pod ends the launch: everything below it is committed
             if (s_rescore) {
                 stop = s;
@@ -244,9 +296,9 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                     done = true;
                 }
             }
-            // a full barrier (with its fence): the next round's picks must see
-            // pod s's update (a bare s_barrier does not wait for the store)
-            __syncthreads();
+            // the next round's picks must see pod s's update (a bare s_barrier
+            // does not wait for the store: round_barrier waits for it)
+            round_barrier<LDS_CAP>();
             // pods below s are done; s itself is done unless it must re-pick
         }
         if (stop < p_end) break;

@@ -20,6 +20,8 @@
 // these pods (capacity only shrinks), so the walk resumes from s unchanged.
 #include "klist.h"
 
+#include <algorithm>
+
 namespace nas {
 namespace {
 
@@ -38,8 +40,10 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
         const int *__restrict__ p0_dev) {
     const int t = blockIdx.x * STALE_THREADS + threadIdx.x;
     const int p = p0 + t;
-    // device-side slot: pods from the halt word on (none when it is < 0)
+    // device-side slot: pods from the halt word on; nothing halted -> k_compact
+    // publishes an empty view without reading the words
     const int first = p0_dev ? *p0_dev : p0;
+    if (first < 0) return;
     bool dry = false;
     if (p < P && first >= 0 && p >= first) {
         const u64 b = bound[p];
@@ -64,9 +68,16 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
 
 __global__ void __launch_bounds__(COMPACT_THREADS)
 k_compact(const u64 *__restrict__ words, int n_words, int p0, int R, int *__restrict__ idx,
-          int *__restrict__ ctl) {
+          int *__restrict__ ctl, const int *__restrict__ p0_dev) {
     __shared__ int part[COMPACT_THREADS];
     const int tid = threadIdx.x;
+    if (p0_dev && *p0_dev < 0) {  // the walk did not halt: empty view
+        if (tid == 0) {
+            ctl[0] = -1;
+            ctl[1] = 0;
+        }
+        return;
+    }
     const int per = (n_words + COMPACT_THREADS - 1) / COMPACT_THREADS;
     const int w0 = min(n_words, tid * per), w1 = min(n_words, w0 + per);
     int c = 0;
@@ -97,19 +108,20 @@ k_compact(const u64 *__restrict__ words, int n_words, int p0, int R, int *__rest
     }
 }
 
-// one workgroup per view row: row i < count copies pod idx[i]'s traffic row
-// and requests
+// view rows i < count (grid-stride, a workgroup per row): pod idx[i]'s
+// traffic row and requests
 __global__ void __launch_bounds__(256)
 k_gather_pods(const int *__restrict__ idx, const int *__restrict__ count, const uint4 *__restrict__ WA,
               int row_vec, const int *__restrict__ req, int Pp, int Rv, uint4 *__restrict__ WA_v,
               int *__restrict__ req_v) {
-    const int i = blockIdx.x;
-    if (i >= *count) return;  // rows past count are scored as garbage and never scattered
-    const int p = idx[i];
-    const uint4 *src = WA + (size_t)p * row_vec;
-    uint4 *dst = WA_v + (size_t)i * row_vec;
-    for (int v = threadIdx.x; v < row_vec; v += 256) dst[v] = src[v];
-    if (threadIdx.x < 3) req_v[threadIdx.x * Rv + i] = req[threadIdx.x * Pp + p];
+    const int n = *count;  // rows past count are scored as garbage and never scattered
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int p = idx[i];
+        const uint4 *src = WA + (size_t)p * row_vec;
+        uint4 *dst = WA_v + (size_t)i * row_vec;
+        for (int v = threadIdx.x; v < row_vec; v += 256) dst[v] = src[v];
+        if (threadIdx.x < 3) req_v[threadIdx.x * Rv + i] = req[threadIdx.x * Pp + p];
+    }
 }
 
 __global__ void k_scatter_lists(const int *__restrict__ idx, const int *__restrict__ count,
@@ -139,7 +151,8 @@ hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t
     k_stale<<<blocks, STALE_THREADS, 0, st>>>(reinterpret_cast<const u64 *>(key),
                                               reinterpret_cast<const u64 *>(bound), req, Pp, cap, N,
                                               p0, P, w, p0_dev);
-    k_compact<<<1, COMPACT_THREADS, 0, st>>>(w, blocks * (STALE_THREADS / 64), p0, R, idx, ctl);
+    k_compact<<<1, COMPACT_THREADS, 0, st>>>(w, blocks * (STALE_THREADS / 64), p0, R, idx, ctl,
+                                             p0_dev);
     return hipGetLastError();
 }
 
@@ -147,7 +160,7 @@ hipError_t launch_gather_pods(hipStream_t st, const int32_t *idx, const int32_t 
                               const void *WA, size_t row_bytes, const int32_t *req, int Pp, int Rv,
                               void *WA_v, int32_t *req_v) {
     if (row_bytes % 16) return hipErrorInvalidValue;
-    k_gather_pods<<<Rv, 256, 0, st>>>(idx, count, static_cast<const uint4 *>(WA),
+    k_gather_pods<<<std::min(Rv, 512), 256, 0, st>>>(idx, count, static_cast<const uint4 *>(WA),
                                       (int)(row_bytes / 16), req, Pp, Rv,
                                       static_cast<uint4 *>(WA_v), req_v);
     return hipGetLastError();
