@@ -64,13 +64,15 @@ namespace {
 constexpr int RESCORE_PODS = 1024;  // pods per device-side rescore slot (multiple of COST_BN)
 constexpr int GATHER_PODS = 4096;   // dry pods rescored per gathered slot (gathered_slot)
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
-// Device-side rescore slots enqueued behind a chunk's commit.  An idle slot
-// still costs its launches a wait for free CUs while scoring fills the chip,
-// and scoring against the live capacity makes stops rare, so by default only
-// the last chunk (nothing left to overlap) gets slots; stops elsewhere are
-// resumed after the pipeline by the host loop.
+constexpr size_t HOST_OUT_OFFSET = 4096;  // pinned staging of nas_place results in host_status
+// Device-side rescore slots enqueued blindly behind a chunk's commit
+// (NAS_RESCORE_SLOTS overrides).  An idle gathered slot still costs ~0.1 ms
+// of launches (C3, measured), more than the host round trip a stop costs once
+// the pipeline is done -- the results fetch brings the halt word back with
+// the placements -- and scoring against the live capacity makes stops rare:
+// by default slots run only for a walk known to have halted.
 constexpr int RESCORE_SLOTS = 0;
-constexpr int RESCORE_SLOTS_LAST = 2;
+constexpr int RESCORE_SLOTS_LAST = 0;
 
 int bind(nas_ctx *ctx) {
     if (!ctx) return NAS_ERR_ARG;
@@ -440,15 +442,19 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
         ctx->timings.cost_launches += 1;
     }
     std::vector<uint32_t> raw;
-    HIPCK(hipMemcpy2DAsync(node_out, (size_t)P * 4, ctx->out_node.p, (size_t)Pp * 4, (size_t)P * 4,
+    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
+    const size_t BP = (size_t)B * P;
+    HIPCK(hipMemcpy2DAsync(stage, (size_t)P * 4, ctx->out_node.p, (size_t)Pp * 4, (size_t)P * 4,
                            B, hipMemcpyDeviceToHost, st));
     if (cost_out || int_score_out) {
-        raw.resize((size_t)B * P);
-        HIPCK(hipMemcpy2DAsync(raw.data(), (size_t)P * 4, ctx->out_cost_i.p, (size_t)Pp * 4,
+        raw.resize(BP);
+        HIPCK(hipMemcpy2DAsync(stage + BP, (size_t)P * 4, ctx->out_cost_i.p, (size_t)Pp * 4,
                                (size_t)P * 4, B, hipMemcpyDeviceToHost, st));
     }
     hipEvent_t t1 = tm.mark(st);
     HIPCK(hipStreamSynchronize(st));
+    std::memcpy(node_out, stage, BP * 4);
+    if (!raw.empty()) std::memcpy(raw.data(), stage + BP, BP * 4);
     tm.span(T_TOTAL, t0, t1);
     int unsched = 0, dev_rounds = 0, rounds = 0;
     for (int b = 0; b < B; ++b) {
@@ -517,7 +523,10 @@ int alloc_extended(nas_ctx *ctx) {
         OK(nas::ensure(ctx, ctx->gather_r, (size_t)ctx->world * RESCORE_PODS * KC * 8));
         OK(nas::ensure(ctx, ctx->gbound_r, (size_t)ctx->world * RESCORE_PODS * 8));
     }
-    const size_t hs_bytes = std::max<size_t>(256, B * nas::STATUS_INTS * 4);
+    // pinned: the status words, then (from HOST_OUT_OFFSET) a staging area for
+    // the placements and scores so their copies back are DMA, not staged
+    const size_t hs_bytes = HOST_OUT_OFFSET + 2 * B * (size_t)ctx->Pp * 4;
+    static_assert(HOST_OUT_OFFSET >= 256, "status words fit below the staging area");
     if (ctx->host_status.bytes < hs_bytes) {
         if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
         ctx->host_status.p = nullptr;
@@ -957,9 +966,27 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
     HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
+    // the results and the walk's status come back in one round trip; only a
+    // walk still halted after the pipeline (rare) needs more slots and another
     int32_t *hs = ctx->host_status.as<int32_t>();
-    HIPCK(hipMemcpyAsync(hs, halt, 4, hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
+    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
+    std::vector<uint32_t> raw(cost_out || int_score_out ? P : 0);
+    hipEvent_t t1 = nullptr;
+    auto fetch = [&]() -> int {
+        // halt[0..2]: halt word, slot resumes, commit rounds; ctl[2]: pods rescored
+        HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(stage, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+        if (!raw.empty())
+            HIPCK(hipMemcpyAsync(stage + P, ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost,
+                                 st));
+        t1 = tm.mark(st);
+        HIPCK(hipStreamSynchronize(st));
+        std::memcpy(node_out, stage, (size_t)P * 4);
+        if (!raw.empty()) std::memcpy(raw.data(), stage + P, (size_t)P * 4);
+        return NAS_OK;
+    };
+    OK(fetch());
     int checks = 0;
     while (hs[0] >= 0) {
         // still halted after the pipeline: more gathered slots, checked in batches
@@ -967,20 +994,8 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         if (++checks > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
         for (int r = 0; r < GATHER_SLOTS_PER_SYNC; ++r)
             OK(gathered_slot(ctx, tm, st, ctx->comm, nullptr, P));
-        HIPCK(hipMemcpyAsync(hs, halt, 4, hipMemcpyDeviceToHost, st));
-        HIPCK(hipStreamSynchronize(st));
+        OK(fetch());
     }
-    // halt[1..2]: slot resumes, commit rounds; ctl[2]: pods rescored by slots
-    HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
-    std::vector<uint32_t> raw;
-    HIPCK(hipMemcpyAsync(node_out, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
-    if (cost_out || int_score_out) {
-        raw.resize(P);
-        HIPCK(hipMemcpyAsync(raw.data(), ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
-    }
-    hipEvent_t t1 = tm.mark();
-    HIPCK(hipStreamSynchronize(st));
     tm.span(T_TOTAL, t0, t1);
     int unsched = 0;
     for (int i = 0; i < P; ++i) {
