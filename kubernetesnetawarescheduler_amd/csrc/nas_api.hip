@@ -492,13 +492,20 @@ int rescore_slots(bool last) {
     return last ? RESCORE_SLOTS_LAST : RESCORE_SLOTS;
 }
 
-// pods per pipelined scoring chunk: at least 32 pod tiles, and enough tiles
-// that one chunk's cost launch has ~512 workgroups on this rank's node tiles
-// (node shards have few node tiles).  The first chunk is always 32 tiles, so
-// the commit stream starts early.
-int chunk_pods(const nas_ctx *ctx, int c) {
+// pods per pipelined scoring chunk starting at pod lo: at least 32 pod
+// tiles, and enough tiles that one chunk's cost launch has ~512 workgroups on
+// this rank's node tiles (node shards have few node tiles).  The first chunk
+// is 32 tiles, so the commit stream starts early, and the last is at most
+// about 32, so the commit left after the scoring ends (the serial tail, which
+// matters most on a node shard's short scoring) is short.
+int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     const int n_mt = ctx->Mp / nas::COST_BM;
-    const int tiles = c == 0 ? 32 : std::max(32, (512 + n_mt - 1) / n_mt);
+    const int big = std::max(32, (512 + n_mt - 1) / n_mt);
+    const int left = (ctx->P - lo + nas::COST_BN - 1) / nas::COST_BN;  // pod tiles left
+    int tiles = c == 0 ? 32 : big;
+    // a big last chunk is split in two so that the last is 32 tiles (unless
+    // the first part would be a sliver of under 16)
+    if (c > 0 && left > 32 && left <= big && left - 32 >= 16) tiles = left - 32;
     return tiles * nas::COST_BN;
 }
 
@@ -949,7 +956,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
     HIPCK(hipStreamWaitEvent(sc, ready, 0));
     for (int c = 0, lo = 0, hi = 0; lo < P; ++c, lo = hi) {
-        hi = std::min(P, lo + chunk_pods(ctx, c));
+        hi = std::min(P, lo + chunk_pods(ctx, c, lo));
         // two scoring streams (each with its own communicator when sharded):
         // a chunk's tail blocks overlap the next chunk
         hipStream_t ss = (c & 1) ? ctx->stream2 : st;
