@@ -386,7 +386,9 @@ def main():
         achieved = ops / (cost_ms * 1e-3) / 1e12
         peak = PEAK_I8_TOPS if args.dtype == "i8" else PEAK_BF16_TFLOPS
         out["roofline"] = {"kernel": "k_cost_topk", "bound": "mfma", "achieved": achieved,
-                           "peak": peak, "unit": "TOPS" if args.dtype == "i8" else "TFLOP/s",
+                           "peak": peak, "unit": "TFLOP/s",
+                           "op_type": "int8 ops (2 per MAC) vs the dense int8 MFMA peak"
+                                      if args.dtype == "i8" else "bf16 FLOPs",
                            "frac": achieved / peak, "traffic": PMC_TRAFFIC.get(("k_cost_topk", args.dtype, N, P, d.world)),
                            "traffic_unit": "B/launch",
                            "launch_ms": cost_ms, "ops_per_launch": ops,

@@ -327,14 +327,9 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
     if (N <= LDS_CAP_MAX_NODES) {
         const size_t lds = 3 * (size_t)N * 4;
-        static bool attr = false;
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_commit<true>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               LDS_DYN_MAX);
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
+        static std::atomic<unsigned long long> attr{0};
+        hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit<true>), LDS_DYN_MAX, attr);
+        if (e != hipSuccess) return e;
         k_commit<true><<<batch, THREADS, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
                                                 oc, halt, nullptr);
     } else {

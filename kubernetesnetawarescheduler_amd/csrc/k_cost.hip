@@ -887,12 +887,9 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const void *fn = m16 ? reinterpret_cast<const void *>(&k_cost_topk16<DT>)
                          : reinterpret_cast<const void *>(&k_cost_topk<DT>);
     const int lds = m16 ? 2 * STAGE_BYTES : lds_bytes<COST_PIPE>();
-    static bool attr_set[2] = {false, false};
-    if (!attr_set[m16]) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
-        attr_set[m16] = true;
-    }
+    static std::atomic<unsigned long long> attr_set[2];
+    hipError_t e = set_lds_once(fn, lds, attr_set[m16]);
+    if (e != hipSuccess) return e;
     const int n_mt = Mp / BM, n_nt = np / BN;
     auto *lt = static_cast<const unsigned char *>(Lt);
     auto *wa = static_cast<const unsigned char *>(WA);

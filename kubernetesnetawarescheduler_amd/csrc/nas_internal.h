@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -107,6 +108,19 @@ struct nas_ctx {
 };
 
 namespace nas {
+
+// hipFuncSetAttribute(max dynamic LDS) once per kernel and device (the
+// attribute is per device; contexts on several devices may share a process)
+inline hipError_t set_lds_once(const void *fn, int bytes, std::atomic<unsigned long long> &done) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+}
 
 int fail(nas_ctx *ctx, int code, const std::string &msg);
 int hip_fail(nas_ctx *ctx, hipError_t e, const char *what);
