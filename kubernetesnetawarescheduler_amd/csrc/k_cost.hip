@@ -60,7 +60,7 @@ constexpr int TILE_BYTES = BM * BKB;          // 32 KiB: one operand, one stage
 template <int PIPE>
 constexpr int lds_bytes() { return PIPE == 1 ? 5 * TILE_BYTES : 2 * STAGE_BYTES; }
 #ifndef COST_SCHED
-#define COST_SCHED 1
+#define COST_SCHED 0
 #endif
 #ifndef COST_MFMA16
 #define COST_MFMA16 0
@@ -122,7 +122,8 @@ struct Top4 {
 // EPI != 0 are diagnostic variants for tools/mb_cost.hip: 1 = accumulators
 // kept alive with an empty asm and no epilogue (times the main loop alone),
 // 2 = per-lane top-1 instead of top-4.  SCHED selects the k-substep schedule
-// (A/B'd in tools/mb_cost.hip): 0 hipcc's own, 1 pinned MFMA/ds_read
+// (A/B'd in tools/mb_cost.hip and on the C3 bench): 0 hipcc's own (the
+// default: ~1% ahead of 1 on the bench, 3 of 3 pairs), 1 pinned MFMA/ds_read
 // interleave, 2 s_setprio(1) around each MFMA cluster, 3 iglp_opt(0),
 // 4 iglp_opt(1).
 template <int DT, int EPI = 0, int SCHED = COST_SCHED, int PIPE = COST_PIPE, int GM = COST_GM>
