@@ -56,6 +56,9 @@ def parse():
                          "one GPU only)")
     ap.add_argument("--c4", action="store_true",
                     help="run C4 (50k nodes x 500k pods, node-sharded) also when --gpus > 1")
+    ap.add_argument("--rccl-world1", action="store_true",
+                    help="diagnostic: at --gpus 1 place through a one-rank RCCL communicator "
+                         "(every chunk's all-gather + cross-rank merge runs)")
     ap.add_argument("--only", choices=["place", "vote", "score"], default=None,
                     help="profile helper: run only one path")
     return ap.parse_args()
@@ -112,7 +115,7 @@ def time_steps(d, fn, steps, warmup):
 
 def bench_place(args, d, eng):
     N, P = args.nodes, args.pods
-    if d.world > 1:
+    if d.world > 1 or args.rccl_world1:
         uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
         eng.comm_init(uid, d.rank, d.world)
     eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
@@ -275,10 +278,32 @@ def config_c1(args, d, eng):
     for s in range(S):
         b, w, _ = oracle.vote(eng.read_snapshot(s), o1, o2)
         ok &= b == best[s] and list(w) == win[s].tolist()
-    return {"workload": f"C1: reference-mode vote, {N} nodes x {S} pods (one snapshot per pod)",
+    # extended mode on the same shape: every pod sends
+    # 100 MB (customNetworkBenchmark/*.data:2) to one bound server pod, seeded
+    # 10 x 10 int8 latency, Raspberry-Pi-sized capacity
+    P = S
+    L = rng.integers(1, 100, (N, N)).astype(np.int8)
+    L = np.triu(L, 1) + np.triu(L, 1).T
+    server = int(rng.integers(0, N))
+    WA = np.zeros((P, N), np.int8)
+    WA[:, server] = 100
+    free = np.tile(np.array([[4000, 4 << 20, 110]], np.int32), (N, 1))
+    req = np.stack([rng.integers(1, 540, P), rng.integers(7_464, 303_749, P), np.ones(P)],
+                   1).astype(np.int32)
+    eng.upload_latency(L, "i8")
+    eng.upload_capacity(free)
+    eng.upload_pods(req)
+    eng.upload_traffic(WA, "i8")
+    te, res = _timed_place(d, eng, args.steps, args.warmup)
+    want, wcost, _ = oracle.place(WA, L, req, free, "i8")
+    ok_ext = (res["node"] == want).all() and (res["score"] == wcost).all()
+    return {"workload": f"C1: reference-mode vote, {N} nodes x {S} pods (one snapshot per pod); "
+                        f"extended mode on the same shape (100 MB per pod to one server pod)",
             "value": S * N / (t / args.steps), "unit": "pair-scores/s",
             "ms_per_step": t * 1e3 / args.steps, "matches_oracle": bool(ok),
-            "note": "launch-latency bound: one score_reference call per step"}
+            "extended": {"ms_per_step": te * 1e3 / args.steps,
+                         "placements_per_s": P / (te / args.steps), "matches_oracle": bool(ok_ext)},
+            "note": "launch-latency bound: one score_reference / nas_place call per step"}
 
 
 def config_c2(args, d, eng):

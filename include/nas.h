@@ -204,7 +204,9 @@ int nas_set_batch(nas_ctx *ctx, int32_t n_clusters);
  * Rank r of `world` owns node columns [r*n/world, (r+1)*n/world) of L; pods,
  * WA and capacities are replicated.  Per-pod candidate lists are exchanged
  * with an RCCL all-gather over xGMI and merged; the commit is replicated, so
- * every rank returns the same placements. */
+ * every rank returns the same placements.  world = 1 builds a real
+ * communicator too (the exchange then runs as a one-rank all-gather: the
+ * whole RCCL path on a single GPU). */
 int nas_comm_unique_id(uint8_t id_out[128]);
 int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world);
 

@@ -89,15 +89,16 @@ int64_t kpad(int n, int dtype) { return nas::round_up(n, dtype == NAS_DT_I8 ? 12
 struct Timer {
     nas_ctx *ctx;
     std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> spans;
-    std::vector<hipEvent_t> evs;
-    explicit Timer(nas_ctx *c) : ctx(c) {}
-    ~Timer() {
-        for (auto e : evs) (void)hipEventDestroy(e);
-    }
+    // events come from the context's pool (every call synchronises before it
+    // returns, so the previous call's events are complete when reused)
+    explicit Timer(nas_ctx *c) : ctx(c) { ctx->ev_used = 0; }
+    ~Timer() { ctx->ev_used = 0; }
     hipEvent_t ev() {
+        if (ctx->ev_used < ctx->ev_pool.size()) return ctx->ev_pool[ctx->ev_used++];
         hipEvent_t e;
         if (hipEventCreate(&e) != hipSuccess) return nullptr;
-        evs.push_back(e);
+        ctx->ev_pool.push_back(e);
+        ctx->ev_used = ctx->ev_pool.size();
         return e;
     }
     hipEvent_t mark(hipStream_t st = nullptr) {
@@ -203,7 +204,9 @@ int exchange(nas_ctx *ctx, ncclComm *cm, hipStream_t st, const uint64_t *keys,
     return NAS_OK;
 }
 
-bool exchanging(const nas_ctx *ctx) { return ctx->world > 1 && !ctx->virtual_shard; }
+// a communicator exchanges even at world 1 (nas_comm_init with world 1
+// builds one: the whole RCCL path on a single GPU, all-gather = copy)
+bool exchanging(const nas_ctx *ctx) { return ctx->comm != nullptr && !ctx->virtual_shard; }
 
 // The pod arrays a scoring pass reads and writes: the context's own, or the
 // gathered scratch view of a rescore (k_rescore.hip) with its own row stride.
@@ -610,6 +613,7 @@ void nas_destroy(nas_ctx *ctx) {
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
     destroy_comms(ctx);
+    for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->stream2);
     (void)hipStreamDestroy(ctx->stream_commit);
@@ -1195,7 +1199,6 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     ctx->rank = rank;
     ctx->world = world;
     ctx->virtual_shard = false;
-    if (world == 1) return NAS_OK;
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
     ncclComm_t comm, comm2 = nullptr, comm_c = nullptr;

@@ -105,6 +105,10 @@ struct nas_ctx {
     ncclComm *comm_c = nullptr;  // rescore slots on `stream_commit`
     int32_t rank = 0, world = 1;
     bool virtual_shard = false;  // nas_set_shard: shard geometry, no exchange
+    // timing events, created once and reused by every call (hipEventCreate
+    // per mark cost a small placement more than its kernels)
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
 };
 
 namespace nas {

@@ -127,3 +127,31 @@ def test_commit_api_stops_and_resumes(engine):
     assert stops and stops == sorted(stops)
     assert node.tolist() == want.tolist() and score.tolist() == wcost.tolist()
     assert (engine.get_capacity() == wfree).all()
+
+
+@pytest.mark.parametrize("P,N,crowd", [(20000, 256, 24), (3000, 1200, 0)])
+def test_rccl_world1_place_equals_oracle(P, N, crowd):
+    """nas_comm_init with world 1 builds real RCCL communicators (one per
+    stream), so every scoring chunk, device-side rescore slot and host-loop
+    rescore goes through ncclAllGather + the cross-rank merge on this GPU.
+    Placements, scores and the capacity left must equal the sequential
+    oracle exactly (the multi-rank collectives themselves run on the driver's
+    8-GPU node; their merge rule is covered by test_shards_merge_*)."""
+    rng = np.random.default_rng(P + N)
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=30, cap_scale=0.6)
+    if crowd:
+        WA[:, :crowd] = 127  # herds on the first nodes: commit stops, rescores
+    with Engine(0) as e:
+        e.comm_init(Engine.comm_unique_id(), 0, 1)
+        e.upload_latency(L, "i8")
+        e.upload_capacity(free)
+        e.upload_pods(req)
+        e.upload_traffic(WA, "i8")
+        for _ in range(2):  # a second pass reuses the communicators
+            e.reset_capacity()
+            node, _, ci = e.place()
+            want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+            assert node.tolist() == want.tolist() and ci.tolist() == wcost.tolist()
+            assert (e.get_capacity() == wfree).all()
+        if crowd:
+            assert e.timings()["rescore_rounds"] > 0
