@@ -57,8 +57,14 @@ constexpr int TILE_BYTES = BM * BKB;          // 32 KiB: one operand, one stage
 // triple-buffered so its loads get two K-steps of cover (160 KiB, all of LDS).
 // PIPE 2: as 0, but B is staged through registers (global_load_dwordx4 ->
 // ds_write_b128) instead of LDS-DMA; PIPE 3: both operands register-staged.
+// PIPE 5 / 6: as 0, plus an L2 "touch" of the stage 2 / 3 K-steps ahead (one
+// 4-byte LDS-DMA per 128-byte line of A and B into a junk LDS word, left in
+// flight across the step's barrier), so the stage's own LDS-DMA one step
+// later hits L2 instead of waiting on HBM / MALL; PIPE 7: as 5, B lines only.
 template <int PIPE>
-constexpr int lds_bytes() { return PIPE == 1 ? 5 * TILE_BYTES : 2 * STAGE_BYTES; }
+constexpr int lds_bytes() {
+    return PIPE == 1 ? 5 * TILE_BYTES : PIPE >= 5 ? 2 * STAGE_BYTES + 256 : 2 * STAGE_BYTES;
+}
 #ifndef COST_SCHED
 #define COST_SCHED 0
 #endif
@@ -97,6 +103,12 @@ __device__ __forceinline__ void glds16(const void *g, void *l) {
                                      (void __attribute__((address_space(3))) *)l, 16, 0, 0);
 }
 
+__device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
+    unsigned d;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 // Per-lane running top-4 as separate (orderable cost, node) u32 words.
 // A lane visits its nodes in ascending node order, so a new (x, n) sorts
 // before entry j iff x < cost[j] strictly (an equal cost has the larger node):
@@ -121,7 +133,9 @@ struct Top4 {
 
 // EPI != 0 are diagnostic variants for tools/mb_cost.hip: 1 = accumulators
 // kept alive with an empty asm and no epilogue (times the main loop alone),
-// 2 = per-lane top-1 instead of top-4.  SCHED selects the k-substep schedule
+// 2 = per-lane top-1 instead of top-4, 6 = the exact Top4 select network
+// only (the default takes the packed med3 path whenever every lane's keys
+// span < 2^26 - 1).  SCHED selects the k-substep schedule
 // (A/B'd in tools/mb_cost.hip and on the C3 bench): 0 hipcc's own (the
 // default: ~1% ahead of 1 on the bench, 3 of 3 pairs), 1 pinned MFMA/ds_read
 // interleave, 2 s_setprio(1) around each MFMA cluster, 3 iglp_opt(0),
@@ -392,6 +406,42 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         step(nk - 1, std::false_type{});
         if (wm == 0) bar();  // re-align the barrier count of the two groups
         __syncthreads();
+    } else if constexpr (PIPE >= 5) {
+        // two-stage pipeline + L2 touch of stage t + D: per step each wave
+        // issues its 8 pieces of stage t+1, then (if any) one touch, and
+        // waits vmcnt(1) -- the pieces and the previous step's touch have
+        // landed, this step's touch stays in flight across the raw barrier
+        constexpr int D = PIPE == 6 ? 3 : 2;
+        unsigned char *junk = lds + 2 * STAGE_BYTES;
+        // PIPE 5/6: threads 0..255 touch A row tid, 256..511 B row tid-256;
+        // PIPE 7: threads 0..255 touch B row tid, the other waves nothing
+        const bool toucher = PIPE != 7 || tid < 256;
+        const unsigned char *trow = (PIPE == 7 || tid >= 256) ? Bg + (size_t)(tid & 255) * Kb
+                                                              : Ag + (size_t)tid * Kb;
+        auto touch = [&](int k0) {
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(trow + k0),
+                                             (void __attribute__((address_space(3))) *)junk, 4, 0, 0);
+        };
+        stageA(0, 0);
+        stageB(0, 0);
+        if (toucher && 1 < nk) touch(BKB);  // stage 1 (its own DMA comes at step 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int t = 0; t < nk; ++t) {
+            const int cur = t & 1;
+            if (t + 1 < nk) {
+                stageA(cur ^ 1, (t + 1) * BKB);
+                stageB(cur ^ 1, (t + 1) * BKB);
+            }
+            const bool tch = toucher && t + D < nk;
+            if (tch) touch((t + D) * BKB);
+            compute(cur, cur, nopiece);
+            if (tch) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        __syncthreads();
     } else if constexpr (PIPE >= 2) {
         // register-staged operands: step t+1's rows are loaded into VGPRs at
         // the top of step t (latency hidden by its MFMAs) and written to the
@@ -487,7 +537,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         __syncthreads();
     }
 
-    if constexpr (EPI == 1 || EPI >= 3) {
+    if constexpr (EPI == 1 || (EPI >= 3 && EPI <= 5)) {
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -505,38 +555,90 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     u64 key[2][8], bnd[2];
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
-        Top4 t4;
-        t4.init();
-        unsigned best1 = 0xffffffffu, bnode1 = 0xffffffffu;
         const int pod = p0 + nt * BN + wn * 64 + ni * 32 + fr;
+        u64 mw[2];
 #pragma unroll
         for (int mi2 = 0; mi2 < 2; ++mi2) {
             const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
-            const u64 mw = mask[(size_t)chunk * Pp + pod];
+            mw[mi2] = mask[(size_t)chunk * Pp + pod];
+        }
+        // orderable keys of the lane's 64 (node, cost) values and their range
+        unsigned u[4][16];
+        unsigned kmin = 0xffffffffu, kmax = 0u;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int mi = mi2 * 2 + h;
-                const unsigned bits = (unsigned)(mw >> (32 * h));
-                const unsigned node0 = (unsigned)(node_base + mt * BM + wm * 128 + mi * 32);
+        for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                for (int reg = 0; reg < 16; ++reg) {
-                    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
-                    // not fitting -> cost all-ones, never inserted (branch-free)
-                    const unsigned x = M::okey(acc[mi][ni][reg]) | ((((bits >> row) & 1u) ^ 1u) * 0xffffffffu);
-                    if constexpr (EPI == 2) {
-                        const bool b = x < best1;
-                        best1 = b ? x : best1;
-                        bnode1 = b ? node0 + row : bnode1;
-                    } else {
-                        t4.insert(x, node0 + row);
+            for (int reg = 0; reg < 16; ++reg) {
+                u[mi][reg] = M::okey(acc[mi][ni][reg]);
+                kmin = min(kmin, u[mi][reg]);
+                kmax = max(kmax, u[mi][reg]);
+            }
+        u64 k4[4];
+        if (EPI == 0 && __all(kmax - kmin < (1u << 26) - 1u)) {
+            // packed path (every lane's keys span < 2^26 - 1): one u32 per
+            // value, (key - kmin) << 6 | i with i = mi*16 + reg increasing in
+            // node order, so u32 order = (cost, node) order; a non-fitting
+            // value is all-ones (never < a fitting one, < 2^32 - 1).  Sorted
+            // insert of x into c0 <= .. <= c3: c3 = med3(c2, c3, x), c2 =
+            // med3(c1, c2, x), c1 = med3(c0, c1, x), c0 = min(c0, x).
+            unsigned c0 = 0xffffffffu, c1 = c0, c2 = c0, c3 = c0;
+#pragma unroll
+            for (int mi2 = 0; mi2 < 2; ++mi2)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int mi = mi2 * 2 + h;
+                    const unsigned nbits = ~(unsigned)(mw[mi2] >> (32 * h));
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg) {
+                        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
+                        unsigned x = ((u[mi][reg] - kmin) << 6) | (unsigned)(mi * 16 + reg);
+                        x |= (unsigned)((int)(nbits << (31 - row)) >> 31);
+                        c3 = umed3(c2, c3, x);
+                        c2 = umed3(c1, c2, x);
+                        c1 = umed3(c0, c1, x);
+                        c0 = min(c0, x);
+                    }
+                }
+            const unsigned cc[4] = {c0, c1, c2, c3};
+            const unsigned nb = (unsigned)(node_base + mt * BM + wm * 128 + 4 * fh);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const unsigned i = cc[j] & 63u, r = i & 15u;
+                const unsigned node = nb + (i >> 4) * 32u + (r & 3u) + 8u * (r >> 2);
+                k4[j] = cc[j] == 0xffffffffu ? KEY_INVALID
+                                             : ((u64)((cc[j] >> 6) + kmin) << 32) | node;
+            }
+        } else {
+            Top4 t4;
+            t4.init();
+            unsigned best1 = 0xffffffffu, bnode1 = 0xffffffffu;
+#pragma unroll
+            for (int mi2 = 0; mi2 < 2; ++mi2) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int mi = mi2 * 2 + h;
+                    const unsigned bits = (unsigned)(mw[mi2] >> (32 * h));
+                    const unsigned node0 = (unsigned)(node_base + mt * BM + wm * 128 + mi * 32);
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg) {
+                        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
+                        // not fitting -> cost all-ones, never inserted (branch-free)
+                        const unsigned x = u[mi][reg] | ((((bits >> row) & 1u) ^ 1u) * 0xffffffffu);
+                        if constexpr (EPI == 2) {
+                            const bool b = x < best1;
+                            best1 = b ? x : best1;
+                            bnode1 = b ? node0 + row : bnode1;
+                        } else {
+                            t4.insert(x, node0 + row);
+                        }
                     }
                 }
             }
-        }
-        if constexpr (EPI == 2) t4.c[0] = best1, t4.n[0] = bnode1;
-        u64 k4[4], o4[4];
+            if constexpr (EPI == 2) t4.c[0] = best1, t4.n[0] = bnode1;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) k4[j] = t4.c[j] == 0xffffffffu ? KEY_INVALID : t4.key(j);
+            for (int j = 0; j < 4; ++j) k4[j] = t4.c[j] == 0xffffffffu ? KEY_INVALID : t4.key(j);
+        }
+        u64 o4[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) o4[j] = shfl_xor64(k4[j], 32);
         merge44(k4, o4, key[ni]);

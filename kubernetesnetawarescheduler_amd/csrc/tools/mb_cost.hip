@@ -41,7 +41,10 @@ int main(int argc, char **argv) {
                       {"top4/jit/regB", KV(0, 0, 2, 4)}, {"top4/jit/regAB", KV(0, 0, 3, 4)},
                       {"noepi/pin/regB", KV(1, 1, 2, 4)}, {"noepi/pin/regAB", KV(1, 1, 3, 4)},
                       {"top4/phased", KV(0, 0, 4, 4)}, {"noepi/phased", KV(1, 0, 4, 4)},
-                      {"top4/phased/g8", KV(0, 0, 4, 8)}, {"top4/phased/g2", KV(0, 0, 4, 2)}};
+                      {"top4/phased/g8", KV(0, 0, 4, 8)}, {"top4/phased/g2", KV(0, 0, 4, 2)},
+                      {"top4/touch2", KV(0, 0, 5, 4)}, {"top4/touch3", KV(0, 0, 6, 4)},
+                      {"top4/touchB2", KV(0, 0, 7, 4)}, {"noepi/touch2", KV(1, 0, 5, 4)},
+                      {"top4sel/jit", KV(6, 0, 0, 4)}};
     const int nv = sizeof(vars) / sizeof(vars[0]);
     for (int v = 0; v < nv; ++v)
         CK(hipFuncSetAttribute(vars[v].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[v].lds));

@@ -101,3 +101,38 @@ def test_bf16_negative_and_zero(engine):
     want, wcost, _ = oracle.place(WA, L, req, free, "bf16")
     assert node.tolist() == want.tolist()
     assert np.allclose(cost, wcost, rtol=1e-5, atol=0)
+
+
+def test_wide_cost_range_exact_select_path(engine):
+    """The cost epilogue keeps a lane's top-4 as packed u32 keys (cost offset
+    << 6 | node slot) only when every lane's 64 costs span < 2^26 - 1, and
+    falls back to the exact (cost, node) select network otherwise.  Here
+    extreme int8 traffic and latency of both signs give costs of +-7e7 next
+    to pods with near-zero traffic (small spans), so waves of both kinds and
+    mixed ties all occur; placements, scores and capacity must equal the
+    oracle exactly, and the candidate lists the oracle's ranking."""
+    rng = np.random.default_rng(77)
+    P, N = 512, 4608
+    sign = np.where(np.arange(N) % 2 == 0, 1, -1)
+    L = (sign[None, :] * rng.integers(120, 128, (N, N))).clip(-128, 127).astype(np.int8)
+    WA = rng.integers(120, 128, (P, N)).astype(np.int8)
+    WA[P // 2:] = rng.integers(-1, 2, (P - P // 2, N)).astype(np.int8)  # small spans
+    WA[3 * P // 4:, 7] = 127  # mixes: one heavy peer on top of the small background
+    free = np.stack([rng.integers(800, 3000, N), rng.integers(800_000, 3_000_000, N),
+                     np.full(N, 3)], 1).astype(np.int32)
+    req = np.stack([rng.integers(1, 540, P), rng.integers(7_464, 303_749, P),
+                    np.ones(P)], 1).astype(np.int32)
+    cost = oracle.cost(WA, L, "i8")
+    assert np.ptp(cost[: P // 2], axis=1).min() > 2**26  # the wide rows really are wide
+    engine.upload_latency(L, "i8")
+    engine.upload_capacity(free)
+    engine.upload_pods(req)
+    engine.upload_traffic(WA, "i8")
+    engine.score()
+    node, ci, _, cnt, _ = engine.candidates()
+    wn, wc, wcnt = oracle.topk(cost, oracle.fit_mask(req, free), 8)
+    assert (cnt >= np.minimum(4, wcnt)).all()
+    for p in range(P):
+        assert node[p, :cnt[p]].tolist() == wn[p, :cnt[p]].tolist(), p
+        assert ci[p, :cnt[p]].tolist() == wc[p, :cnt[p]].tolist(), p
+    run(engine, WA, L, free, req)
