@@ -223,6 +223,19 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         for (int j = 0; j < 4; ++j) pieceB(buf, k0, j);
     };
 
+    // the epilogue's fit-mask words, loaded now so their latency hides
+    // under the main loop (k_fit wrote them before this launch)
+    u64 mwp[2][2];
+    if constexpr (EPI == 0 || EPI == 2 || EPI == 6) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+            for (int mi2 = 0; mi2 < 2; ++mi2) {
+                const int pod = p0 + nt * BN + wn * 64 + ni * 32 + (lane & 31);
+                const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
+                mwp[ni][mi2] = mask[(size_t)chunk * Pp + pod];
+            }
+    }
     acc_t acc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -555,24 +568,30 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     u64 key[2][8], bnd[2];
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) {
-        const int pod = p0 + nt * BN + wn * 64 + ni * 32 + fr;
-        u64 mw[2];
-#pragma unroll
-        for (int mi2 = 0; mi2 < 2; ++mi2) {
-            const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
-            mw[mi2] = mask[(size_t)chunk * Pp + pod];
-        }
+        const u64 *mw = mwp[ni];
         // orderable keys of the lane's 64 (node, cost) values and their range
+        // (int8: the range of the raw int32 costs -- the key is x ^ 2^31, so
+        // key differences are cost differences)
         unsigned u[4][16];
         unsigned kmin = 0xffffffffu, kmax = 0u;
+        int smin = 0x7fffffff, smax = -0x7fffffff - 1;
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
             for (int reg = 0; reg < 16; ++reg) {
-                u[mi][reg] = M::okey(acc[mi][ni][reg]);
-                kmin = min(kmin, u[mi][reg]);
-                kmax = max(kmax, u[mi][reg]);
+                if constexpr (DT == NAS_DT_I8) {
+                    smin = min(smin, (int)acc[mi][ni][reg]);
+                    smax = max(smax, (int)acc[mi][ni][reg]);
+                } else {
+                    u[mi][reg] = M::okey(acc[mi][ni][reg]);
+                    kmin = min(kmin, u[mi][reg]);
+                    kmax = max(kmax, u[mi][reg]);
+                }
             }
+        if constexpr (DT == NAS_DT_I8) {
+            kmin = M::okey(smin);
+            kmax = M::okey(smax);
+        }
         u64 k4[4];
         if (EPI == 0 && __all(kmax - kmin < (1u << 26) - 1u)) {
             // packed path (every lane's keys span < 2^26 - 1): one u32 per
@@ -582,6 +601,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             // insert of x into c0 <= .. <= c3: c3 = med3(c2, c3, x), c2 =
             // med3(c1, c2, x), c1 = med3(c0, c1, x), c0 = min(c0, x).
             unsigned c0 = 0xffffffffu, c1 = c0, c2 = c0, c3 = c0;
+            // int8: raw = cost bits, base = min cost; bf16: raw = key, base = kmin
+            const unsigned nk6 = 0u - ((DT == NAS_DT_I8 ? (unsigned)smin : kmin) << 6);
 #pragma unroll
             for (int mi2 = 0; mi2 < 2; ++mi2)
 #pragma unroll
@@ -591,8 +612,13 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 #pragma unroll
                     for (int reg = 0; reg < 16; ++reg) {
                         const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
-                        unsigned x = ((u[mi][reg] - kmin) << 6) | (unsigned)(mi * 16 + reg);
-                        x |= (unsigned)((int)(nbits << (31 - row)) >> 31);
+                        // (key << 6) - (kmin << 6) = (key - kmin) << 6 (v_lshl_add),
+                        // slot and the sign-extended not-fit bit (v_bfe_i32) OR'ed in
+                        const unsigned raw = DT == NAS_DT_I8 ? (unsigned)(int)acc[mi][ni][reg]
+                                                             : u[mi][reg];
+                        const unsigned x = ((raw << 6) + nk6) |
+                                           (unsigned)(mi * 16 + reg) |
+                                           (unsigned)__builtin_amdgcn_sbfe((int)nbits, row, 1);
                         c3 = umed3(c2, c3, x);
                         c2 = umed3(c1, c2, x);
                         c1 = umed3(c0, c1, x);
@@ -623,7 +649,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                     for (int reg = 0; reg < 16; ++reg) {
                         const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
                         // not fitting -> cost all-ones, never inserted (branch-free)
-                        const unsigned x = u[mi][reg] | ((((bits >> row) & 1u) ^ 1u) * 0xffffffffu);
+                        const unsigned key = DT == NAS_DT_I8 ? M::okey(acc[mi][ni][reg]) : u[mi][reg];
+                        const unsigned x = key | ((((bits >> row) & 1u) ^ 1u) * 0xffffffffu);
                         if constexpr (EPI == 2) {
                             const bool b = x < best1;
                             best1 = b ? x : best1;
