@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--rccl-world1", action="store_true",
                     help="diagnostic: at --gpus 1 place through a one-rank RCCL communicator "
                          "(every chunk's all-gather + cross-rank merge runs)")
+    ap.add_argument("--vote-node-shard", action="store_true",
+                    help="reference mode with the node axis sharded over the ranks (partial "
+                         "records all-gathered over RCCL) instead of pods split across ranks")
     ap.add_argument("--only", choices=["place", "vote", "score"], default=None,
                     help="profile helper: run only one path")
     return ap.parse_args()
@@ -158,8 +161,19 @@ def bench_cost_kernel(args, d, eng):
 
 def bench_vote(args, d, eng):
     N = args.nodes
-    S = args.pods // d.world
-    eng.synth_snapshots(SEED + d.rank, N, S)
+    if args.vote_node_shard:
+        # node axis sharded (SURVEY.md §8(e) vote row): every rank holds its
+        # node slice of all P snapshots; partial records are all-gathered
+        # over RCCL and merged, every rank returns all P decisions
+        S = args.pods
+        lo, hi = d.rank * N // d.world, (d.rank + 1) * N // d.world
+        if not eng.has_comm:
+            uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
+            eng.comm_init(uid, d.rank, d.world)
+        eng.synth_snapshots_shard(SEED, N, lo, hi - lo, S)
+    else:
+        S = args.pods // d.world
+        eng.synth_snapshots(SEED + d.rank, N, S)
     rng = np.random.default_rng(SEED)
     o1 = rng.permutation(N).astype(np.int32)
     o2 = rng.permutation(N + 1).astype(np.int32)
@@ -374,8 +388,19 @@ def run_configs(args, d):
     return out
 
 
+def _claim_stdout():
+    """The contract is ONE JSON line on stdout; RCCL (and HIP runtime libraries)
+    print banners there from native code.  Point fd 1 at stderr for the run and
+    keep the original stdout for the result line."""
+    sys.stdout.flush()
+    keep = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(keep, "w")
+
+
 def main():
     args = parse()
+    result_out = _claim_stdout()
     d = Dist(args.gpus)
     from kubernetesnetawarescheduler_amd import Engine
     eng = Engine(d.local)
@@ -421,18 +446,23 @@ def main():
                                    "(nas_score), HIP events on its stream; 2*P*N*N_local ops"}
     if not args.no_reference_mode and args.only in (None, "vote"):
         elapsed, vote_ms, S, ref = bench_vote(args, d, eng)
-        bytes_launch = 48.0 * N * S
+        pods_total = S if args.vote_node_shard else S * d.world
+        nloc = (d.rank + 1) * N // d.world - d.rank * N // d.world if args.vote_node_shard else N
+        bytes_launch = 48.0 * nloc * S
         out["reference_mode"] = {
-            "value": S * d.world * N / (elapsed / args.steps), "unit": "pair-scores/s",
+            "value": pods_total * N / (elapsed / args.steps), "unit": "pair-scores/s",
             "ms_per_step": elapsed * 1e3 / args.steps,
-            "workload": f"vote scorer, one fresh {N}-node snapshot per pod ({S * d.world} pods)",
-            "roofline": {"kernel": "k_vote", "bound": "hbm",
+            "sharding": "node axis, RCCL all-gather of partial records" if args.vote_node_shard
+                        else "pods (independent snapshots), no collective",
+            "workload": f"vote scorer, one fresh {N}-node snapshot per pod ({pods_total} pods)",
+            "roofline": {"kernel": "k_vote_partial" if args.vote_node_shard else "k_vote",
+                         "bound": "hbm",
                          "achieved": bytes_launch / (vote_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s",
                          "frac": bytes_launch / (vote_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                          "traffic": PMC_TRAFFIC.get(("k_vote", args.dtype, N, P, d.world)),
                          "traffic_unit": "B/launch", "launch_ms": vote_ms, "bytes_per_launch": bytes_launch}}
-        if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline:
+        if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and not args.vote_node_shard:
             out["reference_mode"]["cpu_baseline"] = cpu_baseline_vote(args, eng, ref)
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and gpu_nodes is not None:
         # the vote path freed nothing; re-synthesise the cluster inputs (same seed)
@@ -446,7 +476,7 @@ def main():
         with Engine(d.local) as e:
             out.setdefault("configs", {})["C4"] = config_c4(args, d, e)
     if d.rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
 
 
 if __name__ == "__main__":

@@ -126,6 +126,61 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
                         const int32_t *pod_snapshot, int32_t P, int32_t *best_out,
                         int32_t *winners_out);
 
+/* ---- reference mode, node axis sharded (vote row) --------
+ * Each of the six loops of scheduler.go:334-359 is a first-occurrence
+ * arg-extremum in order1, i.e. a lexicographic (value, pos1) reduction that
+ * splits over node slices.  A shard reduces its slice to one partial record
+ * per snapshot; records of all slices merge in any order into the same six
+ * extrema, from which the net-sent rule (:347-354), the votes (:360-365) and
+ * findBestNode (:384-394) follow.
+ *
+ * Record of one snapshot: six (value, pos1) extrema in the order below;
+ * value = the IEEE-754 bits of the double (cpu, mem, bw) or the int64
+ * (rx, tx, disk) of the first node in order1 holding the extremum among the
+ * slice's nodes that beat the sentinel (:258-265; disk also != 0, :355);
+ * pos1 = that node's position in order1, NAS_VOTE_NOPOS if no node of the
+ * slice qualifies (value then 0). */
+#define NAS_VOTE_NOPOS 0x7fffffff
+#define NAS_VP_CPU 0
+#define NAS_VP_MEM 1
+#define NAS_VP_BW 2
+#define NAS_VP_RX 3
+#define NAS_VP_TX 4
+#define NAS_VP_DISK 5
+typedef struct nas_vote_extremum {
+    int64_t value;
+    int32_t pos1;
+    int32_t reserved; /* 0 */
+} nas_vote_extremum;
+typedef struct nas_vote_partial {
+    nas_vote_extremum m[6]; /* NAS_VP_* */
+} nas_vote_partial;         /* 96 bytes */
+
+/* Upload nodes [node_lo, node_lo + n_local) of n_snapshots snapshots of an
+ * n_nodes-node cluster: field[s * n_local + i] is node node_lo + i.  Orders
+ * (nas_upload_orders / the order arguments) stay over all n_nodes nodes.
+ * With a communicator (nas_comm_init), nas_score_reference on a shard
+ * reduces the slice, all-gathers the partial records over RCCL and merges
+ * them: every rank returns the full result (the ranks' slices must tile
+ * [0, n_nodes) and every rank must make the same call).  Without one, use
+ * nas_vote_partials + nas_vote_merge and move the records yourself. */
+int nas_upload_snapshot_shard(nas_ctx *ctx, const double *cpu, const double *mem,
+                              const int64_t *rx, const int64_t *tx, const double *bw,
+                              const int64_t *disk, int32_t n_nodes, int32_t node_lo,
+                              int32_t n_local, int32_t n_snapshots);
+
+/* Partial records of snapshots [0, S) over this context's node slice (a
+ * whole-cluster snapshot is one slice): out[S].  order1/order2 as in
+ * nas_score_reference (only order1's positions are used here). */
+int nas_vote_partials(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, int32_t S,
+                      nas_vote_partial *out);
+
+/* Merge parts[n_parts * S] (slice-major: parts[k * S + s]) into the decision
+ * of snapshots [0, S) with this context's orders (as nas_score_reference with
+ * pod_snapshot NULL and P = S): best_out[S], winners_out[S * 6] optional. */
+int nas_vote_merge(nas_ctx *ctx, const nas_vote_partial *parts, int32_t n_parts, int32_t S,
+                   int32_t *best_out, int32_t *winners_out);
+
 /* ---- extended mode: fit -> network cost -> top-k -> greedy commit ---------
  *
  * Resources are int32: cpu in millicores, memory in KiB, pod slots.
@@ -261,6 +316,10 @@ int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out
 /* ---- synthetic inputs generated in HBM (benchmarks; seeded, deterministic) */
 /* Reference-mode snapshots per SURVEY.md §8(d) C1/C3. */
 int nas_synth_snapshots(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t n_snapshots);
+/* Nodes [node_lo, node_lo + n_local) of the snapshots nas_synth_snapshots
+ * generates with the same seed and sizes (a node shard of them). */
+int nas_synth_snapshots_shard(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t node_lo,
+                              int32_t n_local, int32_t n_snapshots);
 /* Read back snapshot s (to check sampled pods against a CPU oracle). */
 int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t *rx,
                       int64_t *tx, double *bw, int64_t *disk);

@@ -23,6 +23,9 @@ NAS_EMPTY = -1
 NAS_DT_I8 = 1
 NAS_DT_BF16 = 2
 K_CANDIDATES = 8
+VOTE_NOPOS = 0x7FFFFFFF
+# include/nas.h nas_vote_partial: six (value, pos1, reserved) extrema, NAS_VP_* order
+VOTE_FIELDS = ("cpu", "mem", "bw", "rx", "tx", "disk")
 
 _ERRNAMES = {
     NAS_ERR_ARG: "NAS_ERR_ARG", NAS_ERR_HIP: "NAS_ERR_HIP", NAS_ERR_STATE: "NAS_ERR_STATE",
@@ -69,6 +72,9 @@ SIGNATURES = {
     "nas_upload_snapshot": (_I, [_CTX, _V, _V, _V, _V, _V, _V, _I, _I]),
     "nas_upload_orders": (_I, [_CTX, _V, _V, _I]),
     "nas_score_reference": (_I, [_CTX, _V, _V, _V, _I, _V, _V]),
+    "nas_upload_snapshot_shard": (_I, [_CTX, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I]),
+    "nas_vote_partials": (_I, [_CTX, _V, _V, _I, _V]),
+    "nas_vote_merge": (_I, [_CTX, _V, _I, _I, _V, _V]),
     "nas_upload_latency": (_I, [_CTX, _V, _I, _I]),
     "nas_upload_capacity": (_I, [_CTX, _V, _V, _V, _I]),
     "nas_reset_capacity": (_I, [_CTX]),
@@ -89,6 +95,7 @@ SIGNATURES = {
     "nas_set_candidate_keys": (_I, [_CTX, _I, _I, _V, _V]),
     "nas_commit": (_I, [_CTX, _I, _V, _V, _V, _V]),
     "nas_synth_snapshots": (_I, [_CTX, _c.c_uint64, _I, _I]),
+    "nas_synth_snapshots_shard": (_I, [_CTX, _c.c_uint64, _I, _I, _I, _I]),
     "nas_read_snapshot": (_I, [_CTX, _I, _V, _V, _V, _V, _V, _V]),
     "nas_synth_cluster": (_I, [_CTX, _c.c_uint64, _I, _I, _I, _I]),
     "nas_set_batch": (_I, [_CTX, _I]),

@@ -91,7 +91,7 @@ __device__ __forceinline__ double unit(unsigned long long h) {  // [0, 1)
 // (:444-460) on float32-rounded byte counts; rx/tx ~ U[0, 1e6) with 10% zeros
 // (Atoi failures, :474-478); bw 0 for node 0 ("ubuntu", :287) and 20% of the
 // rest, else U(8e7, 9.5e7) bit/s; disk 0 in 30%, else U[1, 1000].
-__global__ void k_synth_snap(unsigned long long seed, int n, long long ns, int S,
+__global__ void k_synth_snap(unsigned long long seed, int lo, int nl, long long ns, int S,
                              double *__restrict__ cpu, double *__restrict__ mem,
                              double *__restrict__ bw, long long *__restrict__ rx,
                              long long *__restrict__ tx, long long *__restrict__ disk) {
@@ -99,8 +99,9 @@ __global__ void k_synth_snap(unsigned long long seed, int n, long long ns, int S
     for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
          t += (long long)gridDim.x * blockDim.x) {
         const long long s = t / ns;
-        const int node = (int)(t - s * ns);
-        if (node >= n) {  // padding: never wins any comparison
+        const int local = (int)(t - s * ns);
+        const int node = lo + local;  // node index in the whole cluster
+        if (local >= nl) {  // padding: never wins any comparison
             cpu[t] = __longlong_as_double(0x7ff8000000000000ll);
             mem[t] = cpu[t];
             bw[t] = cpu[t];
@@ -295,11 +296,12 @@ hipError_t launch_csr_aggregate(hipStream_t st, const int32_t *row_ptr, const in
     return hipGetLastError();
 }
 
-hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int64_t ns, int S,
-                                  double *cpu, double *mem, double *bw, int64_t *rx, int64_t *tx,
-                                  int64_t *disk) {
+hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int lo, int nl,
+                                  int64_t ns, int S, double *cpu, double *mem, double *bw,
+                                  int64_t *rx, int64_t *tx, int64_t *disk) {
+    (void)n;  // the generator is per (snapshot, node): a slice needs only its bounds
     k_synth_snap<<<grid_for((long long)S * ns, 256), 256, 0, st>>>(
-        seed, n, ns, S, cpu, mem, bw, reinterpret_cast<long long *>(rx),
+        seed, lo, nl, ns, S, cpu, mem, bw, reinterpret_cast<long long *>(rx),
         reinterpret_cast<long long *>(tx), reinterpret_cast<long long *>(disk));
     return hipGetLastError();
 }

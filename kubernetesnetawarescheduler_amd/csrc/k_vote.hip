@@ -56,6 +56,14 @@ struct VoteAcc {
     MaxF bw;
     MinI rx, tx, disk;
     __device__ void init() { cpu.init(); mem.init(); bw.init(); rx.init(); tx.init(); disk.init(); }
+    __device__ void merge(const VoteAcc &b) {
+        if (b.cpu.p != NOPOS) cpu.add(b.cpu.v, b.cpu.p);
+        if (b.mem.p != NOPOS) mem.add(b.mem.v, b.mem.p);
+        if (b.bw.p != NOPOS) bw.add(b.bw.v, b.bw.p);
+        if (b.rx.p != NOPOS) rx.add(b.rx.v, b.rx.p);
+        if (b.tx.p != NOPOS) tx.add(b.tx.v, b.tx.p);
+        if (b.disk.p != NOPOS) disk.add(b.disk.v, b.disk.p);
+    }
     // one node: the six guarded comparisons of scheduler.go:335-355
     __device__ void node(double c, double m, double b, long long r, long long t, long long d, int q) {
         if (c < SENT_CPU) cpu.add(c, q);
@@ -89,32 +97,34 @@ __device__ __forceinline__ void shfl_merge<MinI>(MinI &a, int off) {
     if (q != NOPOS) a.add(x, q);
 }
 
-__global__ void __launch_bounds__(VOTE_THREADS)
-k_vote(const double *__restrict__ cpu, const double *__restrict__ mem,
-       const double *__restrict__ bw, const long long *__restrict__ rx,
-       const long long *__restrict__ tx, const long long *__restrict__ disk, int n, long long ns,
-       const int *__restrict__ order1, const int *__restrict__ pos1,
-       const int *__restrict__ pos2, long long ord_ns, int n_orders,
-       int *__restrict__ best_out, int *__restrict__ win_out) {
-    const int s = blockIdx.x;
+// One snapshot's six extrema over this block's node slice: lanes stream node
+// pairs (16-byte SoA loads), reduce in registers, then wave shuffles and one
+// LDS step across the 4 waves.  The result is valid in thread 0.  Local node
+// i is node lo + i of the cluster; pos1 is indexed by cluster node.
+template <bool SLICE>
+__device__ __forceinline__ VoteAcc reduce_snapshot(
+    const double *__restrict__ cpu, const double *__restrict__ mem, const double *__restrict__ bw,
+    const long long *__restrict__ rx, const long long *__restrict__ tx,
+    const long long *__restrict__ disk, size_t base, int lo, int nl, const int *__restrict__ p1) {
     const int tid = threadIdx.x;
-    const size_t base = (size_t)s * ns;
-    const int o = n_orders == 1 ? 0 : s;
-    const int *p1 = pos1 + (size_t)o * ord_ns;
-
     VoteAcc acc;
     acc.init();
-    // two nodes per lane per step: 16-byte loads of each SoA field (ns is even)
-    for (int i = 2 * tid; i < n; i += 2 * VOTE_THREADS) {
+    for (int i = 2 * tid; i < nl; i += 2 * VOTE_THREADS) {
         const double2 c = *reinterpret_cast<const double2 *>(cpu + base + i);
         const double2 m = *reinterpret_cast<const double2 *>(mem + base + i);
         const double2 b = *reinterpret_cast<const double2 *>(bw + base + i);
         const longlong2 r = *reinterpret_cast<const longlong2 *>(rx + base + i);
         const longlong2 t = *reinterpret_cast<const longlong2 *>(tx + base + i);
         const longlong2 d = *reinterpret_cast<const longlong2 *>(disk + base + i);
-        const int2 q = *reinterpret_cast<const int2 *>(p1 + i);
+        int2 q;
+        if constexpr (SLICE) {  // lo may be odd: two 4-byte loads (pos1 is L2-resident)
+            q.x = p1[lo + i];
+            q.y = i + 1 < nl ? p1[lo + i + 1] : 0;
+        } else {
+            q = *reinterpret_cast<const int2 *>(p1 + i);
+        }
         acc.node(c.x, m.x, b.x, r.x, t.x, d.x, q.x);
-        if (i + 1 < n) acc.node(c.y, m.y, b.y, r.y, t.y, d.y, q.y);
+        if (i + 1 < nl) acc.node(c.y, m.y, b.y, r.y, t.y, d.y, q.y);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
@@ -129,21 +139,22 @@ k_vote(const double *__restrict__ cpu, const double *__restrict__ mem,
     const int wave = tid >> 6;
     if ((tid & 63) == 0) red[wave] = acc;
     __syncthreads();
-    if (tid != 0) return;
     VoteAcc a = red[0];
-    for (int w = 1; w < VOTE_THREADS / 64; ++w) {
-        const VoteAcc &b = red[w];
-        if (b.cpu.p != NOPOS) a.cpu.add(b.cpu.v, b.cpu.p);
-        if (b.mem.p != NOPOS) a.mem.add(b.mem.v, b.mem.p);
-        if (b.bw.p != NOPOS) a.bw.add(b.bw.v, b.bw.p);
-        if (b.rx.p != NOPOS) a.rx.add(b.rx.v, b.rx.p);
-        if (b.tx.p != NOPOS) a.tx.add(b.tx.v, b.tx.p);
-        if (b.disk.p != NOPOS) a.disk.add(b.disk.v, b.disk.p);
+    if (tid == 0) {
+        for (int w = 1; w < VOTE_THREADS / 64; ++w) a.merge(red[w]);
     }
+    return a;
+}
+
+// From the six merged extrema to the decision: net-sent (:347-354), votes
+// (:360-365) and findBestNode over order2 (:384-394).  n = cluster nodes
+// (key n == "none").
+__device__ void vote_decide(const VoteAcc &a, int n, const int *__restrict__ o1,
+                            const int *__restrict__ p2, int *__restrict__ best_out,
+                            int *__restrict__ win_out) {
     // net-sent: the later (in order1) of the tx and bw winners (:347-354)
     int ps = a.tx.p;
     if (a.bw.p != NOPOS && (ps == NOPOS || a.bw.p > ps)) ps = a.bw.p;
-    const int *o1 = order1 + (size_t)o * ord_ns;
     auto node_at = [&](int p) { return p == NOPOS ? n : o1[p]; };  // key n == "none"
     int key[6];
     key[NAS_W_CPU] = node_at(a.cpu.p);
@@ -153,7 +164,6 @@ k_vote(const double *__restrict__ cpu, const double *__restrict__ mem,
     key[NAS_W_BANDWIDTH] = n;  // bestNetBandwith is never assigned (:271, :364)
     key[NAS_W_DISK] = node_at(a.disk.p);
     const int weight[6] = {3, 2, 1, 1, 3, 1};  // :360-365
-    const int *p2 = pos2 + (size_t)o * (ord_ns + 2);
     int best = NAS_EMPTY, best_score = 0, best_pos = NOPOS;
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
@@ -168,11 +178,77 @@ k_vote(const double *__restrict__ cpu, const double *__restrict__ mem,
             best = key[i] == n ? NAS_NONE : key[i];
         }
     }
-    best_out[s] = best;
+    *best_out = best;
     if (win_out) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) win_out[(size_t)s * 6 + i] = key[i] == n ? NAS_NONE : key[i];
+        for (int i = 0; i < 6; ++i) win_out[i] = key[i] == n ? NAS_NONE : key[i];
     }
+}
+
+__global__ void __launch_bounds__(VOTE_THREADS)
+k_vote(const double *__restrict__ cpu, const double *__restrict__ mem,
+       const double *__restrict__ bw, const long long *__restrict__ rx,
+       const long long *__restrict__ tx, const long long *__restrict__ disk, int n, long long ns,
+       const int *__restrict__ order1, const int *__restrict__ pos1,
+       const int *__restrict__ pos2, long long ord_ns, int n_orders,
+       int *__restrict__ best_out, int *__restrict__ win_out) {
+    const int s = blockIdx.x;
+    const int o = n_orders == 1 ? 0 : s;
+    const VoteAcc a = reduce_snapshot<false>(cpu, mem, bw, rx, tx, disk, (size_t)s * ns, 0, n,
+                                             pos1 + (size_t)o * ord_ns);
+    if (threadIdx.x != 0) return;
+    vote_decide(a, n, order1 + (size_t)o * ord_ns, pos2 + (size_t)o * (ord_ns + 2), best_out + s,
+                win_out ? win_out + (size_t)s * 6 : nullptr);
+}
+
+// Node-shard partial: the six extrema of nodes [lo, lo + nl) -> part[s]
+// (include/nas.h nas_vote_partial: value bits, pos1).
+__global__ void __launch_bounds__(VOTE_THREADS)
+k_vote_partial(const double *__restrict__ cpu, const double *__restrict__ mem,
+               const double *__restrict__ bw, const long long *__restrict__ rx,
+               const long long *__restrict__ tx, const long long *__restrict__ disk, int lo,
+               int nl, long long ns, const int *__restrict__ pos1, long long ord_ns,
+               int n_orders, long long *__restrict__ part) {
+    const int s = blockIdx.x;
+    const int o = n_orders == 1 ? 0 : s;
+    const VoteAcc a = reduce_snapshot<true>(cpu, mem, bw, rx, tx, disk, (size_t)s * ns, lo, nl,
+                                            pos1 + (size_t)o * ord_ns);
+    if (threadIdx.x != 0) return;
+    long long *r = part + (size_t)s * 12;
+    const long long v[6] = {__double_as_longlong(a.cpu.v), __double_as_longlong(a.mem.v),
+                            __double_as_longlong(a.bw.v), a.rx.v, a.tx.v, a.disk.v};
+    const int p[6] = {a.cpu.p, a.mem.p, a.bw.p, a.rx.p, a.tx.p, a.disk.p};
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+        r[2 * f] = p[f] == NOPOS ? 0 : v[f];
+        r[2 * f + 1] = (long long)(unsigned)p[f];  // pos1 in the low word, reserved = 0
+    }
+}
+
+// Merge n_parts slices' records per snapshot (one lane per snapshot; the
+// (value, pos1) order is total, so the merge order does not matter), then
+// decide as k_vote does.
+__global__ void __launch_bounds__(256)
+k_vote_merge(const long long *__restrict__ parts, int n_parts, int S, int n,
+             const int *__restrict__ order1, const int *__restrict__ pos2, long long ord_ns,
+             int n_orders, int *__restrict__ best_out, int *__restrict__ win_out) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    VoteAcc a;
+    a.init();
+    for (int k = 0; k < n_parts; ++k) {
+        const long long *r = parts + ((size_t)k * S + s) * 12;
+        const int p[6] = {(int)r[1], (int)r[3], (int)r[5], (int)r[7], (int)r[9], (int)r[11]};
+        if (p[0] != NOPOS) a.cpu.add(__longlong_as_double(r[0]), p[0]);
+        if (p[1] != NOPOS) a.mem.add(__longlong_as_double(r[2]), p[1]);
+        if (p[2] != NOPOS) a.bw.add(__longlong_as_double(r[4]), p[2]);
+        if (p[3] != NOPOS) a.rx.add(r[6], p[3]);
+        if (p[4] != NOPOS) a.tx.add(r[8], p[4]);
+        if (p[5] != NOPOS) a.disk.add(r[10], p[5]);
+    }
+    const int o = n_orders == 1 ? 0 : s;
+    vote_decide(a, n, order1 + (size_t)o * ord_ns, pos2 + (size_t)o * (ord_ns + 2), best_out + s,
+                win_out ? win_out + (size_t)s * 6 : nullptr);
 }
 
 __global__ void k_vote_gather(const int *__restrict__ pod_snap, int P, const int *__restrict__ sb,
@@ -197,6 +273,25 @@ hipError_t launch_vote(hipStream_t st, const nas_ctx *c, int S) {
         c->snap[3].as<long long>(), c->snap[4].as<long long>(), c->snap[5].as<long long>(),
         c->snap_n, c->snap_ns, c->order1.as<int>(), c->pos1.as<int>(), c->pos2.as<int>(),
         c->ord_ns, c->n_orders, c->snap_best.as<int>(), c->snap_win.as<int>());
+    return hipGetLastError();
+}
+
+hipError_t launch_vote_partial(hipStream_t st, const nas_ctx *c, int S, nas_vote_partial *part) {
+    if (S <= 0) return hipSuccess;
+    k_vote_partial<<<S, VOTE_THREADS, 0, st>>>(
+        c->snap[0].as<double>(), c->snap[1].as<double>(), c->snap[2].as<double>(),
+        c->snap[3].as<long long>(), c->snap[4].as<long long>(), c->snap[5].as<long long>(),
+        c->snap_lo, c->snap_nl, c->snap_ns, c->pos1.as<int>(), c->ord_ns, c->n_orders,
+        reinterpret_cast<long long *>(part));
+    return hipGetLastError();
+}
+
+hipError_t launch_vote_merge(hipStream_t st, const nas_ctx *c, const nas_vote_partial *parts,
+                             int n_parts, int S, int32_t *best, int32_t *win) {
+    if (S <= 0) return hipSuccess;
+    k_vote_merge<<<(S + 255) / 256, 256, 0, st>>>(
+        reinterpret_cast<const long long *>(parts), n_parts, S, c->snap_n, c->order1.as<int>(),
+        c->pos2.as<int>(), c->ord_ns, c->n_orders, best, win);
     return hipGetLastError();
 }
 

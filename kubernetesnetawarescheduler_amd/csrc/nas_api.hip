@@ -629,25 +629,121 @@ int nas_get_timings(nas_ctx *ctx, nas_timings *out) {
 }
 
 // ---------------------------------------------------------------- reference
+namespace {
+// Snapshot slice [lo, lo + nl) of an n-node cluster, n_snapshots rows.
+int upload_snapshot_slice(nas_ctx *ctx, const double *cpu, const double *mem, const int64_t *rx,
+                          const int64_t *tx, const double *bw, const int64_t *disk, int32_t n,
+                          int32_t lo, int32_t nl, int32_t n_snapshots, bool sharded) {
+    if (!cpu || !mem || !rx || !tx || !bw || !disk || n <= 0 || nl <= 0 || n_snapshots <= 0)
+        return nas::fail(ctx, NAS_ERR_ARG, "snapshot upload: null array or empty size");
+    if (lo < 0 || (int64_t)lo + nl > n)
+        return nas::fail(ctx, NAS_ERR_ARG, "snapshot upload: node slice outside [0, n_nodes)");
+    const int64_t ns = nas::round_up(nl, 2);
+    const void *src[6] = {cpu, mem, bw, rx, tx, disk};
+    for (int f = 0; f < 6; ++f) {
+        OK(nas::ensure(ctx, ctx->snap[f], (size_t)ns * n_snapshots * 8));
+        HIPCK(hipMemcpy2DAsync(ctx->snap[f].p, ns * 8, src[f], (size_t)nl * 8, (size_t)nl * 8,
+                               n_snapshots, hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (ctx->snap_n != n) ctx->n_orders = 0;  // orders no longer match
+    ctx->snap_n = n;
+    ctx->snap_lo = lo;
+    ctx->snap_nl = nl;
+    ctx->snap_sharded = sharded;
+    ctx->snap_s = n_snapshots;
+    ctx->snap_ns = ns;
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    return NAS_OK;
+}
+
+// nas_score_reference's argument checks and order upload, shared by the
+// node-shard entries.
+int prepare_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2) {
+    if (ctx->snap_s <= 0) return nas::fail(ctx, NAS_ERR_STATE, "no snapshot uploaded");
+    if ((order1 == nullptr) != (order2 == nullptr))
+        return nas::fail(ctx, NAS_ERR_ARG, "order1 and order2 must both be given or both NULL");
+    if (order1) OK(upload_orders(ctx, order1, order2, 1));
+    if (ctx->n_orders != 1 && ctx->n_orders != ctx->snap_s)
+        return nas::fail(ctx, NAS_ERR_STATE, "orders: need 1 set or one per snapshot");
+    return NAS_OK;
+}
+}  // namespace
+
 int nas_upload_snapshot(nas_ctx *ctx, const double *cpu, const double *mem, const int64_t *rx,
                         const int64_t *tx, const double *bw, const int64_t *disk, int32_t n_nodes,
                         int32_t n_snapshots) {
     OK(bind(ctx));
-    if (!cpu || !mem || !rx || !tx || !bw || !disk || n_nodes <= 0 || n_snapshots <= 0)
-        return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_snapshot: null array or empty size");
-    const int64_t ns = nas::round_up(n_nodes, 2);
-    const void *src[6] = {cpu, mem, bw, rx, tx, disk};
-    for (int f = 0; f < 6; ++f) {
-        OK(nas::ensure(ctx, ctx->snap[f], (size_t)ns * n_snapshots * 8));
-        HIPCK(hipMemcpy2DAsync(ctx->snap[f].p, ns * 8, src[f], (size_t)n_nodes * 8,
-                               (size_t)n_nodes * 8, n_snapshots, hipMemcpyHostToDevice,
-                               ctx->stream));
-    }
-    if (ctx->snap_n != n_nodes) ctx->n_orders = 0;  // orders no longer match
-    ctx->snap_n = n_nodes;
-    ctx->snap_s = n_snapshots;
-    ctx->snap_ns = ns;
+    return upload_snapshot_slice(ctx, cpu, mem, rx, tx, bw, disk, n_nodes, 0, n_nodes, n_snapshots,
+                                 false);
+}
+
+int nas_upload_snapshot_shard(nas_ctx *ctx, const double *cpu, const double *mem,
+                              const int64_t *rx, const int64_t *tx, const double *bw,
+                              const int64_t *disk, int32_t n_nodes, int32_t node_lo,
+                              int32_t n_local, int32_t n_snapshots) {
+    OK(bind(ctx));
+    return upload_snapshot_slice(ctx, cpu, mem, rx, tx, bw, disk, n_nodes, node_lo, n_local,
+                                 n_snapshots, true);
+}
+
+int nas_vote_partials(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, int32_t S,
+                      nas_vote_partial *out) {
+    OK(bind(ctx));
+    OK(prepare_orders(ctx, order1, order2));
+    if (S < 0 || S > ctx->snap_s || (S > 0 && !out))
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_vote_partials: S / out");
+    if (S == 0) return NAS_OK;
+    OK(nas::ensure(ctx, ctx->vote_part, (size_t)S * sizeof(nas_vote_partial)));
+    Timer tm(ctx);
+    std::memset(&ctx->timings, 0, sizeof(ctx->timings));
+    hipEvent_t a = tm.mark();
+    HIPCK(nas::launch_vote_partial(ctx->stream, ctx, S, ctx->vote_part.as<nas_vote_partial>()));
+    hipEvent_t b = tm.mark();
+    HIPCK(hipMemcpyAsync(out, ctx->vote_part.p, (size_t)S * sizeof(nas_vote_partial),
+                         hipMemcpyDeviceToHost, ctx->stream));
+    hipEvent_t c = tm.mark();
     HIPCK(hipStreamSynchronize(ctx->stream));
+    tm.span(T_VOTE, a, b);
+    tm.span(T_TOTAL, a, c);
+    ctx->timings.vote_ms = tm.total(T_VOTE);
+    ctx->timings.total_ms = tm.total(T_TOTAL);
+    return NAS_OK;
+}
+
+int nas_vote_merge(nas_ctx *ctx, const nas_vote_partial *parts, int32_t n_parts, int32_t S,
+                   int32_t *best_out, int32_t *winners_out) {
+    OK(bind(ctx));
+    OK(prepare_orders(ctx, nullptr, nullptr));
+    if (n_parts < 1 || S < 0 || (S > 0 && (!parts || !best_out)))
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_vote_merge: parts / n_parts / S / best_out");
+    if (ctx->n_orders != 1 && S > ctx->n_orders)
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_vote_merge: S exceeds the per-snapshot order sets");
+    for (int64_t i = 0; i < (int64_t)n_parts * S; ++i)
+        for (int f = 0; f < 6; ++f) {
+            const int32_t q = parts[i].m[f].pos1;
+            if (q != NAS_VOTE_NOPOS && (q < 0 || q >= ctx->snap_n))
+                return nas::fail(ctx, NAS_ERR_ARG, "nas_vote_merge: pos1 outside [0, n_nodes)");
+        }
+    if (S == 0) return NAS_OK;
+    const size_t pb = (size_t)n_parts * S * sizeof(nas_vote_partial);
+    OK(nas::ensure(ctx, ctx->vote_gather, pb));
+    OK(nas::ensure(ctx, ctx->snap_best, (size_t)S * 4));
+    OK(nas::ensure(ctx, ctx->snap_win, (size_t)S * 24));
+    Timer tm(ctx);
+    std::memset(&ctx->timings, 0, sizeof(ctx->timings));
+    hipEvent_t a = tm.mark();
+    HIPCK(hipMemcpyAsync(ctx->vote_gather.p, parts, pb, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(nas::launch_vote_merge(ctx->stream, ctx, ctx->vote_gather.as<nas_vote_partial>(), n_parts,
+                                 S, ctx->snap_best.as<int32_t>(), ctx->snap_win.as<int32_t>()));
+    HIPCK(hipMemcpyAsync(best_out, ctx->snap_best.p, (size_t)S * 4, hipMemcpyDeviceToHost,
+                         ctx->stream));
+    if (winners_out)
+        HIPCK(hipMemcpyAsync(winners_out, ctx->snap_win.p, (size_t)S * 24, hipMemcpyDeviceToHost,
+                             ctx->stream));
+    hipEvent_t b = tm.mark();
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    tm.span(T_TOTAL, a, b);
+    ctx->timings.total_ms = tm.total(T_TOTAL);
     return NAS_OK;
 }
 
@@ -663,11 +759,11 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
     OK(bind(ctx));
     if (ctx->snap_s <= 0) return nas::fail(ctx, NAS_ERR_STATE, "no snapshot uploaded");
     if (P < 0 || (P > 0 && !best_out)) return nas::fail(ctx, NAS_ERR_ARG, "P / best_out");
-    if ((order1 == nullptr) != (order2 == nullptr))
-        return nas::fail(ctx, NAS_ERR_ARG, "order1 and order2 must both be given or both NULL");
-    if (order1) OK(upload_orders(ctx, order1, order2, 1));
-    if (ctx->n_orders != 1 && ctx->n_orders != ctx->snap_s)
-        return nas::fail(ctx, NAS_ERR_STATE, "orders: need 1 set or one per snapshot");
+    OK(prepare_orders(ctx, order1, order2));
+    if (ctx->snap_sharded && !exchanging(ctx))
+        return nas::fail(ctx, NAS_ERR_STATE,
+                         "node-sharded snapshot: nas_score_reference needs nas_comm_init "
+                         "(or use nas_vote_partials + nas_vote_merge)");
     if (!pod_snapshot && P > ctx->snap_s)
         return nas::fail(ctx, NAS_ERR_ARG, "pod_snapshot NULL needs P <= n_snapshots");
     if (pod_snapshot)
@@ -680,9 +776,27 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
     OK(nas::ensure(ctx, ctx->snap_win, (size_t)S * 6 * 4));
     Timer tm(ctx);
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
-    hipEvent_t a = tm.mark();
-    HIPCK(nas::launch_vote(ctx->stream, ctx, pod_snapshot ? S : P));
-    hipEvent_t b = tm.mark();
+    hipEvent_t a = tm.mark(), b = nullptr;
+    const int Sused = pod_snapshot ? S : P;
+    if (ctx->snap_sharded) {
+        // node shards: partial records of this rank's slice, all-gathered
+        // over RCCL, merged in rank order (every rank gets the full result)
+        const size_t rb = (size_t)Sused * sizeof(nas_vote_partial);
+        OK(nas::ensure(ctx, ctx->vote_part, rb));
+        OK(nas::ensure(ctx, ctx->vote_gather, rb * ctx->world));
+        HIPCK(nas::launch_vote_partial(ctx->stream, ctx, Sused, ctx->vote_part.as<nas_vote_partial>()));
+        b = tm.mark();  // vote_ms: the slice's HBM pass alone
+        ncclResult_t r = ncclAllGather(ctx->vote_part.p, ctx->vote_gather.p, rb, ncclUint8,
+                                       reinterpret_cast<ncclComm_t>(ctx->comm), ctx->stream);
+        if (r != ncclSuccess)
+            return nas::fail(ctx, NAS_ERR_COMM, std::string("vote all-gather: ") + ncclGetErrorString(r));
+        HIPCK(nas::launch_vote_merge(ctx->stream, ctx, ctx->vote_gather.as<nas_vote_partial>(),
+                                     ctx->world, Sused, ctx->snap_best.as<int32_t>(),
+                                     ctx->snap_win.as<int32_t>()));
+    } else {
+        HIPCK(nas::launch_vote(ctx->stream, ctx, Sused));
+        b = tm.mark();
+    }
     const int32_t *best_d = ctx->snap_best.as<int32_t>();
     const int32_t *win_d = ctx->snap_win.as<int32_t>();
     if (pod_snapshot) {
@@ -1249,21 +1363,38 @@ int nas_get_candidate_keys(nas_ctx *ctx, uint64_t *keys, uint64_t *bounds) {
 }
 
 // ---------------------------------------------------------------- synthetic
-int nas_synth_snapshots(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t n_snapshots) {
-    OK(bind(ctx));
-    if (n_nodes <= 0 || n_snapshots <= 0) return nas::fail(ctx, NAS_ERR_ARG, "synth sizes");
-    const int64_t ns = nas::round_up(n_nodes, 2);
+namespace {
+int synth_snapshot_slice(nas_ctx *ctx, uint64_t seed, int32_t n, int32_t lo, int32_t nl,
+                         int32_t n_snapshots, bool sharded) {
+    if (n <= 0 || nl <= 0 || n_snapshots <= 0 || lo < 0 || (int64_t)lo + nl > n)
+        return nas::fail(ctx, NAS_ERR_ARG, "synth sizes / node slice");
+    const int64_t ns = nas::round_up(nl, 2);
     for (int f = 0; f < 6; ++f) OK(nas::ensure(ctx, ctx->snap[f], (size_t)ns * n_snapshots * 8));
-    HIPCK(nas::launch_synth_snapshots(ctx->stream, seed, n_nodes, ns, n_snapshots,
+    HIPCK(nas::launch_synth_snapshots(ctx->stream, seed, n, lo, nl, ns, n_snapshots,
                                       ctx->snap[0].as<double>(), ctx->snap[1].as<double>(),
                                       ctx->snap[2].as<double>(), ctx->snap[3].as<int64_t>(),
                                       ctx->snap[4].as<int64_t>(), ctx->snap[5].as<int64_t>()));
     HIPCK(hipStreamSynchronize(ctx->stream));
-    if (ctx->snap_n != n_nodes) ctx->n_orders = 0;
-    ctx->snap_n = n_nodes;
+    if (ctx->snap_n != n) ctx->n_orders = 0;
+    ctx->snap_n = n;
+    ctx->snap_lo = lo;
+    ctx->snap_nl = nl;
+    ctx->snap_sharded = sharded;
     ctx->snap_s = n_snapshots;
     ctx->snap_ns = ns;
     return NAS_OK;
+}
+}  // namespace
+
+int nas_synth_snapshots(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t n_snapshots) {
+    OK(bind(ctx));
+    return synth_snapshot_slice(ctx, seed, n_nodes, 0, n_nodes, n_snapshots, false);
+}
+
+int nas_synth_snapshots_shard(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t node_lo,
+                              int32_t n_local, int32_t n_snapshots) {
+    OK(bind(ctx));
+    return synth_snapshot_slice(ctx, seed, n_nodes, node_lo, n_local, n_snapshots, true);
 }
 
 int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t *rx, int64_t *tx,
@@ -1274,7 +1405,7 @@ int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t
     for (int f = 0; f < 6; ++f) {
         if (!dst[f]) continue;
         HIPCK(hipMemcpyAsync(dst[f], ctx->snap[f].as<char>() + (size_t)s * ctx->snap_ns * 8,
-                             (size_t)ctx->snap_n * 8, hipMemcpyDeviceToHost, ctx->stream));
+                             (size_t)ctx->snap_nl * 8, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIPCK(hipStreamSynchronize(ctx->stream));
     return NAS_OK;

@@ -52,8 +52,10 @@ struct nas_ctx {
     nas_timings timings = {};
 
     // ---- reference mode
-    int32_t snap_n = 0, snap_s = 0;   // nodes, snapshots
-    int64_t snap_ns = 0;              // padded row stride (even)
+    int32_t snap_n = 0, snap_s = 0;   // nodes (whole cluster), snapshots
+    int32_t snap_lo = 0, snap_nl = 0; // node slice held here: [snap_lo, snap_lo + snap_nl)
+    bool snap_sharded = false;        // uploaded as a node shard (nas_upload_snapshot_shard)
+    int64_t snap_ns = 0;              // padded row stride of the slice (even)
     nas::DevBuf snap[6];              // cpu, mem, bw (f64) ; rx, tx, disk (i64)  [S][ns]
     int32_t n_orders = 0;
     int64_t ord_ns = 0;               // row stride of order arrays
@@ -61,6 +63,7 @@ struct nas_ctx {
     nas::DevBuf order2, pos2;         // [n_orders][ord_ns + 2]  (n+1 keys)
     nas::DevBuf pod_snap, best, winners;
     nas::DevBuf snap_best, snap_win;  // per-snapshot results
+    nas::DevBuf vote_part, vote_gather;  // node-shard partial records [S], [world][S]
 
     // ---- extended mode
     int32_t N = 0;           // nodes
@@ -132,6 +135,11 @@ int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes);
 
 // kernel launchers (k_*.hip); all enqueue on `stream` and return hipError_t
 hipError_t launch_vote(hipStream_t st, const nas_ctx *c, int n_snapshots_used);
+// node-shard form: partial records of the context's slice -> part[S]
+hipError_t launch_vote_partial(hipStream_t st, const nas_ctx *c, int S, nas_vote_partial *part);
+// merge parts[n_parts][S] -> best[S], win[S][6] with the context's orders
+hipError_t launch_vote_merge(hipStream_t st, const nas_ctx *c, const nas_vote_partial *parts,
+                             int n_parts, int S, int32_t *best, int32_t *win);
 hipError_t launch_vote_gather(hipStream_t st, const int32_t *pod_snap, int P,
                               const int32_t *snap_best, const int32_t *snap_win, int32_t *best,
                               int32_t *win);
@@ -193,9 +201,10 @@ hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int 
 hipError_t launch_csr_aggregate(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
                                 const void *w, int dtype, int P, int N, int Kp, void *WA);
 
-hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int64_t ns, int S,
-                                  double *cpu, double *mem, double *bw, int64_t *rx, int64_t *tx,
-                                  int64_t *disk);
+// nodes [lo, lo + nl) of an n-node synthetic snapshot set, row stride ns
+hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int lo, int nl,
+                                  int64_t ns, int S, double *cpu, double *mem, double *bw,
+                                  int64_t *rx, int64_t *tx, int64_t *disk);
 hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
                                 int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
                                 int32_t *cap, int32_t *req, void *L_full /* optional N*N */);

@@ -13,6 +13,8 @@ from . import _lib
 from ._lib import NasError, as_c, ptr
 
 FIELDS = ("cpu", "mem", "rx", "tx", "bw", "disk")
+# one nas_vote_extremum (include/nas.h); a record is 6 of them (NAS_VP_* order)
+VOTE_PARTIAL_DTYPE = np.dtype([("value", "<i8"), ("pos1", "<i4"), ("reserved", "<i4")])
 _FDT = {"cpu": np.float64, "mem": np.float64, "rx": np.int64, "tx": np.int64,
         "bw": np.float64, "disk": np.int64}
 
@@ -30,6 +32,7 @@ class Engine:
         self.n_pods = 0
         self.dtype = 0
         self.n_clusters = 1  # nas_set_batch: arrays carry a leading cluster axis when > 1
+        self.has_comm = False
 
     # ------------------------------------------------------------ plumbing
     def _ck(self, rc):
@@ -71,6 +74,48 @@ class Engine:
                                              ptr(arrs["disk"]), n, S))
         self.snap_nodes, self.snap_count = n, S
 
+    def upload_snapshot_shard(self, snap, n_nodes, node_lo):
+        """Node shard of a snapshot set (include/nas.h nas_upload_snapshot_shard):
+        snap fields are (n_snapshots, n_local) arrays of nodes [node_lo, node_lo+n_local)."""
+        arrs = {f: as_c(snap[f], _FDT[f]) for f in FIELDS}
+        if arrs["cpu"].ndim == 1:
+            arrs = {f: a.reshape(1, -1) for f, a in arrs.items()}
+        S, nl = arrs["cpu"].shape
+        for a in arrs.values():
+            if a.shape != (S, nl):
+                raise ValueError("snapshot fields must share one shape")
+        self._ck(self._L.nas_upload_snapshot_shard(
+            self._h, ptr(arrs["cpu"]), ptr(arrs["mem"]), ptr(arrs["rx"]), ptr(arrs["tx"]),
+            ptr(arrs["bw"]), ptr(arrs["disk"]), n_nodes, node_lo, nl, S))
+        self.snap_nodes, self.snap_count = nl, S
+
+    def synth_snapshots_shard(self, seed, n_nodes, node_lo, n_local, n_snapshots):
+        self._ck(self._L.nas_synth_snapshots_shard(self._h, seed, n_nodes, node_lo, n_local,
+                                                   n_snapshots))
+        self.snap_nodes, self.snap_count = n_local, n_snapshots
+
+    def vote_partials(self, S=None, order1=None, order2=None):
+        """Partial records of this context's node slice: (S, 6) VOTE_PARTIAL_DTYPE."""
+        S = self.snap_count if S is None else S
+        o1 = None if order1 is None else as_c(order1, np.int32)
+        o2 = None if order2 is None else as_c(order2, np.int32)
+        out = np.zeros((S, 6), VOTE_PARTIAL_DTYPE)
+        self._ck(self._L.nas_vote_partials(self._h, ptr(o1), ptr(o2), S, ptr(out)))
+        return out
+
+    def vote_merge(self, parts, winners=True):
+        """parts: (n_parts, S, 6) VOTE_PARTIAL_DTYPE -> best[S], winners[S, 6]."""
+        parts = np.ascontiguousarray(parts, VOTE_PARTIAL_DTYPE)
+        if parts.ndim == 2:
+            parts = parts[None]
+        K, S, six = parts.shape
+        if six != 6:
+            raise ValueError("parts must be (n_parts, S, 6)")
+        best = np.empty(S, np.int32)
+        win = np.empty((S, 6), np.int32) if winners else None
+        self._ck(self._L.nas_vote_merge(self._h, ptr(parts), K, S, ptr(best), ptr(win)))
+        return best, win
+
     def upload_orders(self, order1, order2):
         o1 = as_c(order1, np.int32)
         o2 = as_c(order2, np.int32)
@@ -105,6 +150,7 @@ class Engine:
     def comm_init(self, uid, rank, world):
         b = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
         self._ck(self._L.nas_comm_init(self._h, b, rank, world))
+        self.has_comm = True
 
     def set_shard(self, rank, world):
         self._ck(self._L.nas_set_shard(self._h, rank, world))

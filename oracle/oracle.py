@@ -174,3 +174,104 @@ def commit(cand_node, count, req, free, complete=None):
                     *[_ptr(a) for a in rcols],
                     *[_ptr(a) for a in fcols], _ptr(node), _ptr(slot), ctypes.byref(stop))
     return node, slot, np.stack(fcols, axis=1), stop.value
+
+
+# ---- node-sharded reference mode (SURVEY.md §8(e) vote row, Appendix B) ----
+# Pure-Python/numpy restatement for small cases; records follow include/nas.h
+# nas_vote_partial: six (value bits, pos1) extrema in the order
+# cpu, mem, bw, rx, tx, disk; pos1 = NOPOS when no node of the slice beats
+# the sentinel (value then 0).
+NOPOS = 0x7FFFFFFF
+PART_FIELDS = ("cpu", "mem", "bw", "rx", "tx", "disk")
+# sentinels scheduler.go:258-265 (bw omitted -> 0.0); guards of :335-355
+_SENT = {"cpu": 99999999999.0, "mem": 99999999999.0, "rx": 99999999999,
+         "tx": 99999999999, "disk": 999, "bw": 0.0}
+_IS_MAX = {"bw"}
+_IS_F64 = {"cpu", "mem", "bw"}
+
+
+def _bits(x, f):
+    if f in _IS_F64:
+        return int(np.array([x], np.float64).view(np.int64)[0])
+    return int(x)
+
+
+def _unbits(v, f):
+    if f in _IS_F64:
+        return float(np.array([v], np.int64).view(np.float64)[0])
+    return int(v)
+
+
+def _qualifies(x, f):
+    # scheduler.go:335 / :339 / :343 / :347 (<), :351 (> 0.0), :355 (< 999 && != 0)
+    if f == "bw":
+        return x > _SENT[f]
+    if f == "disk":
+        return x != 0 and x < _SENT[f]
+    return x < _SENT[f]
+
+
+def _better(x, q, v, p, f):
+    """(x, q) beats the kept (v, p): strictly better value, or a value that is
+    neither better nor worse (equal; -0.0 == +0.0) at an earlier pos1."""
+    if p == NOPOS:
+        return True
+    if f in _IS_MAX:
+        return x > v or (not (v > x) and q < p)
+    return x < v or (not (v < x) and q < p)
+
+
+def vote_partial(metrics, node_lo, order1):
+    """Partial record of nodes [node_lo, node_lo + len) of one snapshot:
+    list of six (value_bits, pos1).  metrics: dict of the slice's arrays."""
+    n_all = len(order1)
+    pos1 = np.empty(n_all, np.int64)
+    pos1[np.asarray(order1, np.int64)] = np.arange(n_all)
+    rec = []
+    for f in PART_FIELDS:
+        vals = np.asarray(metrics[f], np.float64 if f in _IS_F64 else np.int64)
+        v, p = 0, NOPOS
+        for i in range(vals.shape[0]):
+            x = vals[i].item()
+            q = int(pos1[node_lo + i])
+            if _qualifies(x, f) and _better(x, q, v, p, f):
+                v, p = x, q
+        rec.append((_bits(v, f) if p != NOPOS else 0, p))
+    return rec
+
+
+def vote_from_partials(parts, order1, order2):
+    """Merge the records of every slice of one snapshot, then net-sent
+    (scheduler.go:347-354), votes (:360-365) and findBestNode (:384-394).
+    Returns (best, winners[6])."""
+    n = len(order1)
+    keep = {}
+    for f_i, f in enumerate(PART_FIELDS):
+        v, p = 0, NOPOS
+        for rec in parts:
+            bits, q = rec[f_i]
+            if q == NOPOS:
+                continue
+            x = _unbits(bits, f)
+            if _better(x, q, v, p, f):
+                v, p = x, q
+        keep[f] = p
+    ps = keep["tx"]
+    if keep["bw"] != NOPOS and (ps == NOPOS or keep["bw"] > ps):
+        ps = keep["bw"]
+
+    def node_at(q):
+        return n if q == NOPOS else int(order1[q])
+
+    key = [node_at(keep["cpu"]), node_at(keep["mem"]), node_at(ps), node_at(keep["rx"]),
+           n, node_at(keep["disk"])]
+    weight = [3, 2, 1, 1, 3, 1]
+    scores = {}
+    for k, w in zip(key, weight):
+        scores[k] = scores.get(k, 0) + w
+    maxp, best = 0, EMPTY
+    for k in order2:
+        sc = scores.get(int(k), 0)
+        if sc > maxp:
+            maxp, best = sc, (NONE if k == n else int(k))
+    return best, [NONE if k == n else k for k in key]
