@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--vote-node-shard", action="store_true",
                     help="reference mode with the node axis sharded over the ranks (partial "
                          "records all-gathered over RCCL) instead of pods split across ranks")
+    ap.add_argument("--rehearse-world", type=int, default=0,
+                    help="diagnostic at --gpus 1: time rank 0 of a G-GPU node-sharded pass "
+                         "(its node columns; the other ranks' lists are shifted copies of its "
+                         "own; placements not meaningful, RCCL over a one-rank communicator)")
     ap.add_argument("--only", choices=["place", "vote", "score"], default=None,
                     help="profile helper: run only one path")
     return ap.parse_args()
@@ -118,18 +122,30 @@ def time_steps(d, fn, steps, warmup):
 
 def bench_place(args, d, eng):
     N, P = args.nodes, args.pods
-    if d.world > 1 or args.rccl_world1:
+    if args.rehearse_world > 1:
+        assert d.world == 1, "--rehearse-world runs on one GPU"
+        os.environ["NAS_REHEARSE_WORLD"] = str(args.rehearse_world)
+    if d.world > 1 or args.rccl_world1 or args.rehearse_world > 1:
         uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
         eng.comm_init(uid, d.rank, d.world)
+        os.environ.pop("NAS_REHEARSE_WORLD", None)
     eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+    if args.rehearse_world > 1:
+        # the stand-in lists repeat this rank's few best nodes G times, so
+        # herds would drain them at once; with 64x capacity no list runs dry
+        # and the pass times scoring + exchange + merge + the full commit walk
+        eng.upload_capacity(np.minimum(eng.get_capacity().astype(np.int64) * 64,
+                                       2**31 - 1).astype(np.int32))
     keys = ("cost_ms", "fit_ms", "merge_ms", "commit_ms", "total_ms", "cost_launches",
             "rescore_rounds", "unschedulable")
     acc = dict.fromkeys(keys, 0.0)
     state = {"node": None}
+    # placements and integer scores come back every step (into reused arrays)
+    outs = (np.empty(P, np.int32), None, np.empty(P, np.int64))
 
     def step():
         eng.reset_capacity()
-        node, _, score = eng.place(want_cost=True)
+        node, _, score = eng.place(out=outs)
         t = eng.timings()
         for k in keys:
             acc[k] += t[k]
@@ -416,6 +432,10 @@ def main():
                       "nodes": N, "pods": P, "parallelism": f"node-sharded x{d.world}",
                       "candidates_per_pod": 8}}
     gpu_nodes = None
+    if args.rehearse_world > 1:
+        out["rehearsal"] = (f"rank 0 of a {args.rehearse_world}-GPU node-sharded pass on one GPU: "
+                            "its node columns scored, the other ranks' lists stood in for by "
+                            "shifted copies; NOT a multi-GPU measurement, placements not checked")
     if args.only not in ("vote", "score"):
         elapsed, per, gpu_nodes = bench_place(args, d, eng)
         out["value"] = P * N / (elapsed / args.steps)
@@ -431,7 +451,7 @@ def main():
         if gpu_nodes is None:
             eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
         cost_ms, samples = bench_cost_kernel(args, d, eng)
-        nloc = N // d.world
+        nloc = N // max(d.world, args.rehearse_world)
         ops = 2.0 * P * N * nloc
         achieved = ops / (cost_ms * 1e-3) / 1e12
         peak = PEAK_I8_TOPS if args.dtype == "i8" else PEAK_BF16_TFLOPS

@@ -267,7 +267,46 @@ inline int grid_for(long long total, int threads) {
     return (int)(g < 65536 ? (g > 0 ? g : 1) : 65536);
 }
 
+__global__ void k_pass_init(int *__restrict__ status, const int *__restrict__ cap,
+                            int *__restrict__ cap_snap, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < 2 * STATUS_INTS) status[t] = t == 0 ? -1 : 0;
+    if (cap_snap)
+        for (int i = t; i < n; i += gridDim.x * blockDim.x) cap_snap[i] = cap[i];
+}
+
+__global__ void k_rehearse_replicate(unsigned long long *__restrict__ gk,
+                                     unsigned long long *__restrict__ gb, long long nk,
+                                     long long nb, int G, int N) {
+    const long long n = nk + nb;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n;
+         t += (long long)gridDim.x * blockDim.x) {
+        const bool is_key = t < nk;
+        const long long i = is_key ? t : t - nk;
+        unsigned long long *a = is_key ? gk : gb;
+        const long long stride = is_key ? nk : nb;
+        const unsigned long long k = a[i];
+        for (int r = 1; r < G; ++r)
+            a[r * stride + i] = k == ~0ull ? k : k + (unsigned long long)((long long)r * N / G);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
+                            int n) {
+    k_pass_init<<<cap_snap ? grid_for(n, 256) : 1, 256, 0, st>>>(status, cap, cap_snap, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *gk, uint64_t *gb, size_t np, int G,
+                                     int N) {
+    const long long nk = (long long)np * KC, nb = (long long)np;
+    k_rehearse_replicate<<<grid_for(nk + nb, 256), 256, 0, st>>>(
+        reinterpret_cast<unsigned long long *>(gk), reinterpret_cast<unsigned long long *>(gb), nk,
+        nb, G, N);
+    return hipGetLastError();
+}
 
 hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
                               int nloc, int Mp, int Kp, void *Lt) {

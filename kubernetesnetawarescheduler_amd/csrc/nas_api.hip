@@ -201,6 +201,8 @@ int exchange(nas_ctx *ctx, ncclComm *cm, hipStream_t st, const uint64_t *keys,
     if (r == ncclSuccess) r = r2;
     if (r != ncclSuccess)
         return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    if (ctx->rehearse > 1)
+        HIPCK(nas::launch_rehearse_replicate(st, gk, gb, np, ctx->rehearse, ctx->N));
     return NAS_OK;
 }
 
@@ -222,10 +224,35 @@ PodView main_view(nas_ctx *ctx) {
             ctx->cand_bound.as<uint64_t>()};
 }
 
+// merge of pods [p_lo, p_hi)'s node-tile lists (-> exchange over `cm` and
+// merge across ranks), on stream st behind their cost launch; gbuf picks the
+// gathered-list scratch (one per stream that exchanges)
+int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, ncclComm *cm,
+                int gbuf, const PodView &v) {
+    const int pr0 = p_lo / nas::COST_BN * nas::COST_BN;
+    const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
+    const int np = pr1 - pr0;
+    hipEvent_t e2 = tm.mark(st);
+    const int n_lists = ctx->Mp / nas::COST_BM;
+    HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
+                            (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, v.key, v.bound));
+    if (exchanging(ctx)) {
+        // exchange the per-shard lists of pods [pr0, pr1) and merge across ranks
+        auto *gk = ctx->gather[gbuf].as<uint64_t>();
+        auto *gb = ctx->gbound[gbuf].as<uint64_t>();
+        OK(exchange(ctx, cm, st, v.key + (size_t)pr0 * KC, v.bound + pr0, (size_t)np, gk, gb));
+        HIPCK(nas::launch_merge(st, gk, gb, ctx->world, (int64_t)np * KC, np, pr0, p_lo,
+                                p_hi - p_lo, v.key, v.bound));
+    }
+    tm.span(T_MERGE, e2, tm.mark(st));
+    return NAS_OK;
+}
+
 // scoring for pods [p_lo, p_hi) on stream st against capacity `cap`:
-// fit -> cost/top-k -> merge (-> exchange over the stream's communicator)
+// fit -> cost/top-k, then (merge = true) merge_range on the same stream over
+// the stream's communicator
 int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nullptr,
-                const int32_t *cap = nullptr, const PodView *view = nullptr) {
+                const int32_t *cap = nullptr, const PodView *view = nullptr, bool merge = true) {
     if (!st) st = ctx->stream;
     if (!cap) cap = ctx->cap.as<int32_t>();
     const PodView v = view ? *view : main_view(ctx);
@@ -242,23 +269,10 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
                                 mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
                                 ctx->Nloc0));
     hipEvent_t e2 = tm.mark(st);
-    const int n_lists = ctx->Mp / nas::COST_BM;
-    HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
-                            (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, v.key, v.bound));
-    if (exchanging(ctx)) {
-        // exchange the per-shard lists of pods [pr0, pr1) and merge across ranks
-        auto *gk = ctx->gather[sidx].as<uint64_t>();
-        auto *gb = ctx->gbound[sidx].as<uint64_t>();
-        OK(exchange(ctx, sidx ? ctx->comm2 : ctx->comm, st, v.key + (size_t)pr0 * KC, v.bound + pr0,
-                    (size_t)np, gk, gb));
-        HIPCK(nas::launch_merge(st, gk, gb, ctx->world, (int64_t)np * KC, np, pr0, p_lo,
-                                p_hi - p_lo, v.key, v.bound));
-    }
-    hipEvent_t e3 = tm.mark(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
-    tm.span(T_MERGE, e2, e3);
     ctx->timings.cost_launches += 1;
+    if (merge) OK(merge_range(ctx, tm, p_lo, p_hi, st, sidx ? ctx->comm2 : ctx->comm, sidx, v));
     return NAS_OK;
 }
 
@@ -495,6 +509,16 @@ int rescore_slots(bool last) {
     return last ? RESCORE_SLOTS_LAST : RESCORE_SLOTS;
 }
 
+// where a chunk's merge / exchange runs in nas_place: on the commit stream
+// (default) or behind its cost launch on the scoring stream (NAS_MERGE_ON=score)
+bool merge_on_commit_stream() {
+    static const bool v = [] {
+        const char *e = std::getenv("NAS_MERGE_ON");
+        return !(e && std::strcmp(e, "score") == 0);
+    }();
+    return v;
+}
+
 // pods per pipelined scoring chunk starting at pod lo: at least 32 pod
 // tiles, and enough tiles that one chunk's cost launch has ~512 workgroups on
 // this rank's node tiles (node shards have few node tiles).  The first chunk
@@ -502,13 +526,33 @@ int rescore_slots(bool last) {
 // about 32, so the commit left after the scoring ends (the serial tail, which
 // matters most on a node shard's short scoring) is short.
 int chunk_pods(const nas_ctx *ctx, int c, int lo) {
+    static const int wgs = [] {
+        const char *e = std::getenv("NAS_CHUNK_WG");  // tuning knob: workgroups per big chunk
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 512;
+    }();
+    static const int env_mode = [] {
+        const char *e = std::getenv("NAS_CHUNK_MODE");  // tuning knob, see below
+        return e ? std::atoi(e) : -1;
+    }();
     const int n_mt = ctx->Mp / nas::COST_BM;
-    const int big = std::max(32, (512 + n_mt - 1) / n_mt);
+    const int big = std::max(32, (wgs + n_mt - 1) / n_mt);
+    // 32-tile chunks (whole waves of workgroups at 8+ node tiles) with a
+    // short last one; when the workgroup target sets the size (a node shard
+    // with few node tiles), equal chunks: on rank 0 of a G = 8 rehearsal
+    // 1.45 ms vs 1.56 ms per C3 pass, while at G = 1 the 32-tile form is
+    // 2.5% ahead (8.15 vs 8.37 ms)
+    const int mode = env_mode >= 0 ? env_mode : (big > 32 ? 2 : 0);
     const int left = (ctx->P - lo + nas::COST_BN - 1) / nas::COST_BN;  // pod tiles left
     int tiles = c == 0 ? 32 : big;
-    // a big last chunk is split in two so that the last is 32 tiles (unless
-    // the first part would be a sliver of under 16)
-    if (c > 0 && left > 32 && left <= big && left - 32 >= 16) tiles = left - 32;
+    if (mode == 0) {
+        // a big last chunk is split in two so that the last is 32 tiles (unless
+        // the first part would be a sliver of under 16)
+        if (c > 0 && left > 32 && left <= big && left - 32 >= 16) tiles = left - 32;
+    } else if (mode == 2 && c > 0) {
+        // the rest in equal chunks of at most `big` tiles
+        const int n = (left + big - 1) / big;
+        tiles = (left + n - 1) / n;
+    }
     return tiles * nas::COST_BN;
 }
 
@@ -782,8 +826,9 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
         // node shards: partial records of this rank's slice, all-gathered
         // over RCCL, merged in rank order (every rank gets the full result)
         const size_t rb = (size_t)Sused * sizeof(nas_vote_partial);
+        const int ranks = ctx->rehearse > 1 ? 1 : ctx->world;  // the communicator's size
         OK(nas::ensure(ctx, ctx->vote_part, rb));
-        OK(nas::ensure(ctx, ctx->vote_gather, rb * ctx->world));
+        OK(nas::ensure(ctx, ctx->vote_gather, rb * ranks));
         HIPCK(nas::launch_vote_partial(ctx->stream, ctx, Sused, ctx->vote_part.as<nas_vote_partial>()));
         b = tm.mark();  // vote_ms: the slice's HBM pass alone
         ncclResult_t r = ncclAllGather(ctx->vote_part.p, ctx->vote_gather.p, rb, ncclUint8,
@@ -791,7 +836,7 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
         if (r != ncclSuccess)
             return nas::fail(ctx, NAS_ERR_COMM, std::string("vote all-gather: ") + ncclGetErrorString(r));
         HIPCK(nas::launch_vote_merge(ctx->stream, ctx, ctx->vote_gather.as<nas_vote_partial>(),
-                                     ctx->world, Sused, ctx->snap_best.as<int32_t>(),
+                                     ranks, Sused, ctx->snap_best.as<int32_t>(),
                                      ctx->snap_win.as<int32_t>()));
     } else {
         HIPCK(nas::launch_vote(ctx->stream, ctx, Sused));
@@ -1065,11 +1110,17 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     const bool live_cap = nas::commit_in_lds(N);
     const int32_t *score_cap = live_cap ? ctx->cap.as<int32_t>() : ctx->cap_snap.as<int32_t>();
     int32_t *pub = live_cap ? nullptr : ctx->cap_snap.as<int32_t>();
-    if (!live_cap)
-        HIPCK(hipMemcpyAsync(ctx->cap_snap.p, ctx->cap.p, (size_t)3 * N * 4, hipMemcpyDeviceToDevice, st));
-    HIPCK(hipMemsetAsync(halt, 0xff, 4, st));  // halt = -1
-    HIPCK(hipMemsetAsync(halt + 1, 0, 8, st));  // device-side rescores, commit rounds
-    HIPCK(hipMemsetAsync(halt + nas::STATUS_INTS, 0, 16, st));  // gathered-slot control
+    // one launch: halt = -1, rescores / rounds / slot control = 0 (and the
+    // published capacity for the L2 commit) -- three memsets and a copy cost
+    // ~60 us of serial enqueue before the first chunk
+    HIPCK(nas::launch_pass_init(st, halt, live_cap ? nullptr : ctx->cap.as<int32_t>(),
+                                live_cap ? nullptr : ctx->cap_snap.as<int32_t>(), 3 * N));
+    int32_t *hs = ctx->host_status.as<int32_t>();
+    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
+    const bool want_raw = cost_out || int_score_out;
+    const uint32_t *raw = reinterpret_cast<const uint32_t *>(stage + P);  // decoded in place
+    struct Landed { int lo, hi; hipEvent_t ev; };
+    std::vector<Landed> landed;
     hipEvent_t ready = tm.mark(st);
     HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
     HIPCK(hipStreamWaitEvent(sc, ready, 0));
@@ -1078,8 +1129,18 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         // two scoring streams (each with its own communicator when sharded):
         // a chunk's tail blocks overlap the next chunk
         hipStream_t ss = (c & 1) ? ctx->stream2 : st;
-        OK(score_range(ctx, tm, lo, hi, ss, score_cap));
-        HIPCK(hipStreamWaitEvent(sc, tm.mark(ss), 0));
+        if (merge_on_commit_stream()) {
+            // the scoring streams run fit + cost only, back to back; the
+            // commit stream merges (and exchanges, over its own
+            // communicator) each chunk right before committing it, so no
+            // scoring launch waits behind a merge or an all-gather
+            OK(score_range(ctx, tm, lo, hi, ss, score_cap, nullptr, false));
+            HIPCK(hipStreamWaitEvent(sc, tm.mark(ss), 0));
+            OK(merge_range(ctx, tm, lo, hi, sc, ctx->comm_c, 0, main_view(ctx)));
+        } else {
+            OK(score_range(ctx, tm, lo, hi, ss, score_cap));
+            HIPCK(hipStreamWaitEvent(sc, tm.mark(ss), 0));
+        }
         hipEvent_t c0 = tm.mark(sc);
         HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
@@ -1088,30 +1149,54 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         tm.span(T_COMMIT, c0, tm.mark(sc));
         for (int r = 0, n = rescore_slots(hi == P); r < n; ++r)
             OK(gathered_slot(ctx, tm, sc, ctx->comm_c, pub, hi));
+        // this chunk's results go to the pinned stage right behind its
+        // commit, and the host unpacks them while later chunks still run
+        HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo, (size_t)(hi - lo) * 4,
+                             hipMemcpyDeviceToHost, sc));
+        if (want_raw)
+            HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
+                                 (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, sc));
+        landed.push_back({lo, hi, tm.mark(sc)});
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
     HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
-    // the results and the walk's status come back in one round trip; only a
-    // walk still halted after the pipeline (rare) needs more slots and another
-    int32_t *hs = ctx->host_status.as<int32_t>();
-    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
-    std::vector<uint32_t> raw(cost_out || int_score_out ? P : 0);
     hipEvent_t t1 = nullptr;
     auto fetch = [&]() -> int {
         // halt[0..2]: halt word, slot resumes, commit rounds; ctl[2]: pods rescored
         HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
         HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
         HIPCK(hipMemcpyAsync(stage, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
-        if (!raw.empty())
+        if (want_raw)
             HIPCK(hipMemcpyAsync(stage + P, ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost,
                                  st));
         t1 = tm.mark(st);
         HIPCK(hipStreamSynchronize(st));
-        std::memcpy(node_out, stage, (size_t)P * 4);
-        if (!raw.empty()) std::memcpy(raw.data(), stage + P, (size_t)P * 4);
         return NAS_OK;
     };
-    OK(fetch());
+    int unsched = 0;
+    auto unpack = [&](int lo, int hi) {
+        std::memcpy(node_out + lo, stage + lo, (size_t)(hi - lo) * 4);
+        for (int i = lo; i < hi; ++i) {
+            const bool none = node_out[i] < 0;
+            unsched += none;
+            if (cost_out) cost_out[i] = none ? 0.f : decode_cost(raw[i], ctx->dtype);
+            if (int_score_out)
+                int_score_out[i] = (none || ctx->dtype != NAS_DT_I8)
+                                       ? 0 : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
+        }
+    };
+    // the walk's status comes back in one round trip on `st`; meanwhile the
+    // host unpacks each chunk as its copy lands.  Values copied behind a commit
+    // are final unless the walk halted there -- then (rare) more slots run and
+    // everything is fetched and unpacked again.
+    HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
+    t1 = tm.mark(st);
+    for (const Landed &l : landed) {
+        HIPCK(hipEventSynchronize(l.ev));
+        unpack(l.lo, l.hi);
+    }
+    HIPCK(hipStreamSynchronize(st));
     int checks = 0;
     while (hs[0] >= 0) {
         // still halted after the pipeline: more gathered slots, checked in batches
@@ -1120,17 +1205,12 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         for (int r = 0; r < GATHER_SLOTS_PER_SYNC; ++r)
             OK(gathered_slot(ctx, tm, st, ctx->comm, nullptr, P));
         OK(fetch());
+        if (hs[0] < 0) {
+            unsched = 0;
+            unpack(0, P);
+        }
     }
     tm.span(T_TOTAL, t0, t1);
-    int unsched = 0;
-    for (int i = 0; i < P; ++i) {
-        const bool none = node_out[i] < 0;
-        unsched += none;
-        if (cost_out) cost_out[i] = none ? 0.f : decode_cost(raw[i], ctx->dtype);
-        if (int_score_out)
-            int_score_out[i] = (none || ctx->dtype != NAS_DT_I8) ? 0
-                                                                : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
-    }
     ctx->timings.fit_ms = tm.total(T_FIT);
     ctx->timings.cost_ms = tm.total(T_COST);
     ctx->timings.merge_ms = tm.total(T_MERGE);
@@ -1313,6 +1393,11 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     ctx->rank = rank;
     ctx->world = world;
     ctx->virtual_shard = false;
+    ctx->rehearse = 0;
+    if (const char *g = std::getenv("NAS_REHEARSE_WORLD"); g && world == 1 && std::atoi(g) > 1) {
+        ctx->rehearse = std::atoi(g);  // diagnostic: one rank of a G-GPU pass (nas_internal.h)
+        ctx->world = ctx->rehearse;
+    }
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
     ncclComm_t comm, comm2 = nullptr, comm_c = nullptr;

@@ -107,6 +107,11 @@ struct nas_ctx {
     ncclComm *comm2 = nullptr;   // scoring chunks on `stream2`
     ncclComm *comm_c = nullptr;  // rescore slots on `stream_commit`
     int32_t rank = 0, world = 1;
+    // diagnostic (NAS_REHEARSE_WORLD=G with a one-rank communicator): shard
+    // geometry of rank 0 of G, the other G-1 ranks' lists stood in for by
+    // copies of this rank's shifted to their node ranges -- times one rank of
+    // a G-GPU pass on a single GPU; placements are not meaningful
+    int32_t rehearse = 0;
     bool virtual_shard = false;  // nas_set_shard: shard geometry, no exchange
     // timing events, created once and reused by every call (hipEventCreate
     // per mark cost a small placement more than its kernels)
@@ -196,6 +201,14 @@ hipError_t launch_scatter_lists(hipStream_t st, const int32_t *idx, const int32_
                                 const uint64_t *key_v, const uint64_t *bound_v, uint64_t *key,
                                 uint64_t *bound);
 
+// start of a nas_place pass: status[0] = -1 (halt), status[1 .. 2*STATUS_INTS)
+// = 0; cap_snap[0, n) = cap[0, n) when cap_snap is non-null
+hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
+                            int n);
+// rehearsal: slots 1..G-1 of gathered lists [G][np*KC] / bounds [G][np] =
+// slot 0 with node indices shifted to rank r's first node (r * N / G)
+hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *gk, uint64_t *gb, size_t np, int G,
+                                     int N);
 hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
                               int nloc, int Mp, int Kp, void *Lt);
 hipError_t launch_csr_aggregate(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,

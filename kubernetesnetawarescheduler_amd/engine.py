@@ -279,11 +279,21 @@ class Engine:
                                             ptr(complete)))
         return node, ci, cf, cnt, complete.astype(bool)
 
-    def place(self, want_cost=True):
+    def place(self, want_cost=True, out=None):
+        """-> (node, float cost, integer score) per pod.  out: optional
+        (node int32, cost float32 or None, score int64 or None) arrays of
+        length B*P to fill instead of fresh ones (repeated calls then touch no
+        new pages)."""
         B, P = self.n_clusters, self.n_pods
-        node = np.empty(B * P, np.int32)
-        cf = np.empty(B * P, np.float32) if want_cost else None
-        ci = np.empty(B * P, np.int64) if want_cost else None
+        if out is not None:
+            node, cf, ci = out
+            for a, dt in ((node, np.int32), (cf, np.float32), (ci, np.int64)):
+                if a is not None and (a.dtype != dt or a.size != B * P or not a.flags.c_contiguous):
+                    raise ValueError("place(out=...): wrong dtype, size or layout")
+        else:
+            node = np.empty(B * P, np.int32)
+            cf = np.empty(B * P, np.float32) if want_cost else None
+            ci = np.empty(B * P, np.int64) if want_cost else None
         self._ck(self._L.nas_place(self._h, ptr(node), ptr(cf), ptr(ci)))
         if B > 1:
             node = node.reshape(B, P)
