@@ -106,6 +106,13 @@ struct Timer {
         if (e) (void)hipEventRecord(e, st ? st : ctx->stream);
         return e;
     }
+    // a timing-only mark: none when stage timings are off (NAS_STAGE_TIMINGS=0,
+    // read per call), so the pass records only the events it synchronises on
+    bool fine_on = [] {
+        const char *e = std::getenv("NAS_STAGE_TIMINGS");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    hipEvent_t fine(hipStream_t st = nullptr) { return fine_on ? mark(st) : nullptr; }
     void span(int which, hipEvent_t a, hipEvent_t b) { spans.push_back({which, {a, b}}); }
     float total(int which) {
         float s = 0;
@@ -232,7 +239,7 @@ int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, ncc
     const int pr0 = p_lo / nas::COST_BN * nas::COST_BN;
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
     const int np = pr1 - pr0;
-    hipEvent_t e2 = tm.mark(st);
+    hipEvent_t e2 = tm.fine(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
                             (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, v.key, v.bound));
@@ -244,7 +251,7 @@ int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, ncc
         HIPCK(nas::launch_merge(st, gk, gb, ctx->world, (int64_t)np * KC, np, pr0, p_lo,
                                 p_hi - p_lo, v.key, v.bound));
     }
-    tm.span(T_MERGE, e2, tm.mark(st));
+    tm.span(T_MERGE, e2, tm.fine(st));
     return NAS_OK;
 }
 
@@ -261,14 +268,14 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
     const int np = pr1 - pr0;
     auto *mask = ctx->mask.as<uint64_t>();
-    hipEvent_t e0 = tm.mark(st);
+    hipEvent_t e0 = tm.fine(st);
     HIPCK(nas::launch_fit(st, cap, ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp, v.req, p_hi, v.Pp, p_lo,
                           p_hi - p_lo, mask));
-    hipEvent_t e1 = tm.mark(st);
+    hipEvent_t e1 = tm.fine(st);
     HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, v.WA, ctx->Mp, ctx->Kp, v.Pp, pr0, np,
                                 mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
                                 ctx->Nloc0));
-    hipEvent_t e2 = tm.mark(st);
+    hipEvent_t e2 = tm.fine(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
     ctx->timings.cost_launches += 1;
@@ -507,6 +514,16 @@ int rescore_slots(bool last) {
     }();
     if (n >= 0) return n;
     return last ? RESCORE_SLOTS_LAST : RESCORE_SLOTS;
+}
+
+// copy each chunk's results to the host right behind its commit (default)
+// or all of them at the end (NAS_CHUNK_COPIES=0)
+bool chunk_copies() {
+    static const bool v = [] {
+        const char *e = std::getenv("NAS_CHUNK_COPIES");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return v;
 }
 
 // where a chunk's merge / exchange runs in nas_place: on the commit stream
@@ -1141,22 +1158,24 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
             OK(score_range(ctx, tm, lo, hi, ss, score_cap));
             HIPCK(hipStreamWaitEvent(sc, tm.mark(ss), 0));
         }
-        hipEvent_t c0 = tm.mark(sc);
+        hipEvent_t c0 = tm.fine(sc);
         HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
                                  1, pub));
-        tm.span(T_COMMIT, c0, tm.mark(sc));
+        tm.span(T_COMMIT, c0, tm.fine(sc));
         for (int r = 0, n = rescore_slots(hi == P); r < n; ++r)
             OK(gathered_slot(ctx, tm, sc, ctx->comm_c, pub, hi));
         // this chunk's results go to the pinned stage right behind its
         // commit, and the host unpacks them while later chunks still run
+        if (chunk_copies()) {
         HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo, (size_t)(hi - lo) * 4,
                              hipMemcpyDeviceToHost, sc));
         if (want_raw)
             HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
                                  (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, sc));
         landed.push_back({lo, hi, tm.mark(sc)});
+        }
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
     HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
@@ -1191,7 +1210,15 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // everything is fetched and unpacked again.
     HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
+    if (landed.empty()) {  // NAS_CHUNK_COPIES=0: one copy of everything at the end
+        HIPCK(hipMemcpyAsync(stage, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+        if (want_raw)
+            HIPCK(hipMemcpyAsync(stage + P, ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost,
+                                 st));
+        landed.push_back({0, P, nullptr});
+    }
     t1 = tm.mark(st);
+    if (!landed.back().ev) landed.back().ev = t1;
     for (const Landed &l : landed) {
         HIPCK(hipEventSynchronize(l.ev));
         unpack(l.lo, l.hi);
