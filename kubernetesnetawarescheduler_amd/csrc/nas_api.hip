@@ -1141,23 +1141,33 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     hipEvent_t ready = tm.mark(st);
     HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
     HIPCK(hipStreamWaitEvent(sc, ready, 0));
-    for (int c = 0, lo = 0, hi = 0; lo < P; ++c, lo = hi) {
-        hi = std::min(P, lo + chunk_pods(ctx, c, lo));
+    // chunk bounds; every scoring launch is enqueued before any commit-stream
+    // work, so the host's enqueue time of merges / commits / copies never
+    // delays the next chunk's cost launch
+    std::vector<std::pair<int, int>> chunks;
+    for (int c = 0, lo = 0; lo < P; ++c) {
+        const int hi = std::min(P, lo + chunk_pods(ctx, c, lo));
+        chunks.push_back({lo, hi});
+        lo = hi;
+    }
+    const bool split = merge_on_commit_stream();
+    std::vector<hipEvent_t> scored(chunks.size());
+    auto score_chunk = [&](size_t c) -> int {
         // two scoring streams (each with its own communicator when sharded):
         // a chunk's tail blocks overlap the next chunk
         hipStream_t ss = (c & 1) ? ctx->stream2 : st;
-        if (merge_on_commit_stream()) {
-            // the scoring streams run fit + cost only, back to back; the
-            // commit stream merges (and exchanges, over its own
-            // communicator) each chunk right before committing it, so no
-            // scoring launch waits behind a merge or an all-gather
-            OK(score_range(ctx, tm, lo, hi, ss, score_cap, nullptr, false));
-            HIPCK(hipStreamWaitEvent(sc, tm.mark(ss), 0));
-            OK(merge_range(ctx, tm, lo, hi, sc, ctx->comm_c, 0, main_view(ctx)));
-        } else {
-            OK(score_range(ctx, tm, lo, hi, ss, score_cap));
-            HIPCK(hipStreamWaitEvent(sc, tm.mark(ss), 0));
-        }
+        OK(score_range(ctx, tm, chunks[c].first, chunks[c].second, ss, score_cap, nullptr, !split));
+        scored[c] = tm.mark(ss);
+        return NAS_OK;
+    };
+    if (split)  // fit + cost only: the commit stream merges (and exchanges, over
+                // its own communicator) each chunk right before committing it
+        for (size_t c = 0; c < chunks.size(); ++c) OK(score_chunk(c));
+    for (size_t c = 0; c < chunks.size(); ++c) {
+        const int lo = chunks[c].first, hi = chunks[c].second;
+        if (!split) OK(score_chunk(c));
+        HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
+        if (split) OK(merge_range(ctx, tm, lo, hi, sc, ctx->comm_c, 0, main_view(ctx)));
         hipEvent_t c0 = tm.fine(sc);
         HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
@@ -1169,12 +1179,12 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         // this chunk's results go to the pinned stage right behind its
         // commit, and the host unpacks them while later chunks still run
         if (chunk_copies()) {
-        HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo, (size_t)(hi - lo) * 4,
-                             hipMemcpyDeviceToHost, sc));
-        if (want_raw)
-            HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
+            HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo,
                                  (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, sc));
-        landed.push_back({lo, hi, tm.mark(sc)});
+            if (want_raw)
+                HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
+                                     (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, sc));
+            landed.push_back({lo, hi, tm.mark(sc)});
         }
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
