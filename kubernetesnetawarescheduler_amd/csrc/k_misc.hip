@@ -275,19 +275,12 @@ __global__ void k_pass_init(int *__restrict__ status, const int *__restrict__ ca
         for (int i = t; i < n; i += gridDim.x * blockDim.x) cap_snap[i] = cap[i];
 }
 
-__global__ void k_rehearse_replicate(unsigned long long *__restrict__ gk,
-                                     unsigned long long *__restrict__ gb, long long nk,
-                                     long long nb, int G, int N) {
-    const long long n = nk + nb;
-    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n;
-         t += (long long)gridDim.x * blockDim.x) {
-        const bool is_key = t < nk;
-        const long long i = is_key ? t : t - nk;
-        unsigned long long *a = is_key ? gk : gb;
-        const long long stride = is_key ? nk : nb;
+__global__ void k_rehearse_replicate(unsigned long long *__restrict__ a, long long n, int G, int N) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
         const unsigned long long k = a[i];
         for (int r = 1; r < G; ++r)
-            a[r * stride + i] = k == ~0ull ? k : k + (unsigned long long)((long long)r * N / G);
+            a[r * n + i] = k == ~0ull ? k : k + (unsigned long long)((long long)r * N / G);
     }
 }
 
@@ -299,12 +292,9 @@ hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap,
     return hipGetLastError();
 }
 
-hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *gk, uint64_t *gb, size_t np, int G,
-                                     int N) {
-    const long long nk = (long long)np * KC, nb = (long long)np;
-    k_rehearse_replicate<<<grid_for(nk + nb, 256), 256, 0, st>>>(
-        reinterpret_cast<unsigned long long *>(gk), reinterpret_cast<unsigned long long *>(gb), nk,
-        nb, G, N);
+hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *buf, size_t n, int G, int N) {
+    k_rehearse_replicate<<<grid_for((long long)n, 256), 256, 0, st>>>(
+        reinterpret_cast<unsigned long long *>(buf), (long long)n, G, N);
     return hipGetLastError();
 }
 

@@ -6,6 +6,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -208,8 +210,10 @@ int exchange(nas_ctx *ctx, ncclComm *cm, hipStream_t st, const uint64_t *keys,
     if (r == ncclSuccess) r = r2;
     if (r != ncclSuccess)
         return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
-    if (ctx->rehearse > 1)
-        HIPCK(nas::launch_rehearse_replicate(st, gk, gb, np, ctx->rehearse, ctx->N));
+    if (ctx->rehearse > 1) {
+        HIPCK(nas::launch_rehearse_replicate(st, gk, np * KC, ctx->rehearse, ctx->N));
+        HIPCK(nas::launch_rehearse_replicate(st, gb, np, ctx->rehearse, ctx->N));
+    }
     return NAS_OK;
 }
 
@@ -241,15 +245,28 @@ int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, ncc
     const int np = pr1 - pr0;
     hipEvent_t e2 = tm.fine(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
-    HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
-                            (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, v.key, v.bound));
-    if (exchanging(ctx)) {
-        // exchange the per-shard lists of pods [pr0, pr1) and merge across ranks
-        auto *gk = ctx->gather[gbuf].as<uint64_t>();
-        auto *gb = ctx->gbound[gbuf].as<uint64_t>();
-        OK(exchange(ctx, cm, st, v.key + (size_t)pr0 * KC, v.bound + pr0, (size_t)np, gk, gb));
-        HIPCK(nas::launch_merge(st, gk, gb, ctx->world, (int64_t)np * KC, np, pr0, p_lo,
-                                p_hi - p_lo, v.key, v.bound));
+    if (!exchanging(ctx)) {
+        HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
+                                n_lists, (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, v.key,
+                                v.bound));
+    } else {
+        // this rank's lists of pods [pr0, pr1) go straight into one send
+        // buffer ([np][8] keys, then [np] bounds), so one all-gather moves
+        // them; the cross-rank merge reads the rank-major result in place
+        const size_t seg = (size_t)np * (KC + 1);
+        OK(nas::ensure(ctx, ctx->xsend[gbuf], seg * 8));
+        auto *xs = ctx->xsend[gbuf].as<uint64_t>();
+        auto *gx = ctx->gather[gbuf].as<uint64_t>();
+        HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
+                                n_lists, (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, xs,
+                                xs + (size_t)np * KC, pr0));
+        ncclResult_t r = ncclAllGather(xs, gx, seg, ncclUint64, reinterpret_cast<ncclComm_t>(cm), st);
+        if (r != ncclSuccess)
+            return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        if (ctx->rehearse > 1)
+            HIPCK(nas::launch_rehearse_replicate(st, gx, seg, ctx->rehearse, ctx->N));
+        HIPCK(nas::launch_merge(st, gx, gx + (size_t)np * KC, ctx->world, (int64_t)seg,
+                                (int64_t)seg, pr0, p_lo, p_hi - p_lo, v.key, v.bound));
     }
     tm.span(T_MERGE, e2, tm.fine(st));
     return NAS_OK;
@@ -586,7 +603,7 @@ int alloc_extended(nas_ctx *ctx) {
     OK(nas::ensure(ctx, ctx->cap_snap, (size_t)3 * ctx->N * 4));
     if (exchanging(ctx)) {
         for (int i = 0; i < 2; ++i) {
-            OK(nas::ensure(ctx, ctx->gather[i], (size_t)ctx->world * ctx->Pp * KC * 8));
+            OK(nas::ensure(ctx, ctx->gather[i], (size_t)ctx->world * ctx->Pp * (KC + 1) * 8));
             OK(nas::ensure(ctx, ctx->gbound[i], (size_t)ctx->world * ctx->Pp * 8));
         }
         OK(nas::ensure(ctx, ctx->resc_key, (size_t)RESCORE_PODS * KC * 8));
@@ -669,7 +686,8 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->resc_key, &ctx->resc_bound, &ctx->gather_r, &ctx->gbound_r,
                       &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
                       &ctx->g_words, &ctx->g_idx, &ctx->g_WA, &ctx->g_req, &ctx->g_key,
-                      &ctx->g_bound, &ctx->g_gk, &ctx->g_gb, &ctx->status, &ctx->scratch};
+                      &ctx->g_bound, &ctx->g_gk, &ctx->g_gb, &ctx->status, &ctx->scratch,
+                      &ctx->vote_part, &ctx->vote_gather, &ctx->xsend[0], &ctx->xsend[1]};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
@@ -1112,6 +1130,8 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     if (ctx->B > 1) return place_batch(ctx, tm, node_out, cost_out, int_score_out);
+    static const bool trace_host = std::getenv("NAS_TRACE_HOST") != nullptr;  // diagnostic
+    const auto h0 = std::chrono::steady_clock::now();
     hipStream_t st = ctx->stream, sc = ctx->stream_commit;
     const int P = ctx->P, N = ctx->N;
     int32_t *halt = ctx->status.as<int32_t>();
@@ -1189,6 +1209,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
     HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
+    const auto h1 = std::chrono::steady_clock::now();
     hipEvent_t t1 = nullptr;
     auto fetch = [&]() -> int {
         // halt[0..2]: halt word, slot resumes, commit rounds; ctl[2]: pods rescored
@@ -1234,6 +1255,12 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         unpack(l.lo, l.hi);
     }
     HIPCK(hipStreamSynchronize(st));
+    if (trace_host) {
+        const auto h2 = std::chrono::steady_clock::now();
+        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        std::fprintf(stderr, "nas_place host: enqueue %.1f us, wait+unpack %.1f us, chunks %zu\n",
+                     us(h0, h1), us(h1, h2), chunks.size());
+    }
     int checks = 0;
     while (hs[0] >= 0) {
         // still halted after the pipeline: more gathered slots, checked in batches

@@ -63,7 +63,8 @@ struct nas_ctx {
     nas::DevBuf order2, pos2;         // [n_orders][ord_ns + 2]  (n+1 keys)
     nas::DevBuf pod_snap, best, winners;
     nas::DevBuf snap_best, snap_win;  // per-snapshot results
-    nas::DevBuf vote_part, vote_gather;  // node-shard partial records [S], [world][S]
+    nas::DevBuf vote_part, vote_gather;
+    nas::DevBuf xsend[2];  // per gather slot: a chunk's lists to all-gather, [np][8] keys | [np] bounds  // node-shard partial records [S], [world][S]
 
     // ---- extended mode
     int32_t N = 0;           // nodes
@@ -205,10 +206,10 @@ hipError_t launch_scatter_lists(hipStream_t st, const int32_t *idx, const int32_
 // = 0; cap_snap[0, n) = cap[0, n) when cap_snap is non-null
 hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
                             int n);
-// rehearsal: slots 1..G-1 of gathered lists [G][np*KC] / bounds [G][np] =
-// slot 0 with node indices shifted to rank r's first node (r * N / G)
-hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *gk, uint64_t *gb, size_t np, int G,
-                                     int N);
+// rehearsal: rank slots 1..G-1 of an all-gathered buffer [G][n] of keys
+// (or bounds) = slot 0 with node indices shifted to rank r's first node
+// (r * N / G); ~0 stays
+hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *buf, size_t n, int G, int N);
 hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
                               int nloc, int Mp, int Kp, void *Lt);
 hipError_t launch_csr_aggregate(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
