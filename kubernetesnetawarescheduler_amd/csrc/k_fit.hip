@@ -5,27 +5,28 @@
 // Kubernetes NodeResourcesFit rule: pod p fits node n iff
 // req[r][p] <= free[r][n] for r in {cpu millicores, memory KiB, pod slots}.
 //
-// Layout: lane-per-pod.  A block owns 256 consecutive pods (one per lane;
-// requests in VGPRs, one coalesced read) and FIT_CHUNKS 64-node chunks, whose
-// capacities it stages once in LDS (SoA, padding nodes = -1 so they never
-// fit).  Per node, the wave reads the node's three capacities with
-// wave-uniform (broadcast) ds_read_b128s, three v_cmp give the fit lane mask
-// and one shift-and-add folds it into the lane's 32-bit word (nodes visited
-// high to low, so bit j ends up as node j).  Every lane then holds its pod's
-// 64-bit word for the chunk and the wave writes them with one coalesced
-// 8-byte-per-lane store:
+// Layout: lane-per-NODE.  Each wave owns one 64-node chunk c (lane j = node
+// 64c + j, its three free capacities in VGPRs, read once) and walks pods:
+// a pod's requests are wave-uniform (wide scalar loads of 64 pods at a
+// time), three v_cmp against
+// the lanes' capacities and their AND are the pod's 64-bit fit word for the
+// chunk directly -- the ballot -- which v_writelane drops into lane i of the
+// group's result, so 64 pods end in one coalesced 8-byte-per-lane store:
 //   mask[c * Pp + p]  bit j  <=>  pod p fits local node 64c + j.
-// ~5 VALU per 64 pairs: the kernel runs near the speed of its mask write
+// ~8 instructions per (pod, 64 nodes) instead of ~6 per (pod, node) in a
+// lane-per-pod form: the kernel runs at the rate of its mask write
 // (P*N/8 bytes, HBM) -- see DESIGN.md.
 #include "nas_internal.h"
 
 namespace nas {
 namespace {
 
-constexpr int FIT_THREADS = 256;  // 4 waves = 256 pods per block
-constexpr int FIT_CHUNKS = 8;     // 512 nodes per block
+// 16 ints at 4-byte alignment: one s_load_dwordx16 from a uniform address
+typedef int v16i_a4 __attribute__((ext_vector_type(16), aligned(4)));
 
-typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int FIT_THREADS = 256;  // 4 waves = 4 node chunks per block
+constexpr int FIT_WAVES = FIT_THREADS / 64;
+constexpr int FIT_PODS = 512;     // pods per block (8 groups of 64)
 
 __global__ void __launch_bounds__(FIT_THREADS)
 k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
@@ -37,51 +38,62 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
         p0 = s;
         if (dyn_hi_ptr) p_end = dyn_hi_ptr[blockIdx.z * STATUS_INTS];
         p_end = min(p_end, s + dyn_win);
-        if (p0 + (int)blockIdx.x * FIT_THREADS >= p_end) return;  // whole block
     }
+    const int pb0 = p0 + (int)blockIdx.x * FIT_PODS;
+    if (pb0 >= p_end) return;  // whole block (no barriers below)
     const int cb = blockIdx.z;  // cluster of a batched launch
     cap += (size_t)cb * 3 * N;
     req += (size_t)cb * 3 * Pp;
     mask += (size_t)cb * n_chunks * Pp;
-    __shared__ __attribute__((aligned(16))) int sc[3][FIT_CHUNKS * 64];
-    const int tid = threadIdx.x;
-    const int c0 = blockIdx.y * FIT_CHUNKS;
-    const int c1 = min(n_chunks, c0 + FIT_CHUNKS);
-    for (int i = tid; i < FIT_CHUNKS * 64; i += FIT_THREADS) {
-        const int nl = c0 * 64 + i;
-        const bool real = nl < nloc;
-        // relaxed atomic loads: nas_place filters against the working
-        // capacity while the commit stream publishes into it
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-            sc[r][i] = real ? __hip_atomic_load(const_cast<int *>(cap) + (size_t)r * N + n0 + nl, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT)
-                            : -1;
+    const int lane = threadIdx.x & 63;
+    const int c = (int)blockIdx.y * FIT_WAVES + (int)(threadIdx.x >> 6);
+    if (c >= n_chunks) return;
+    const int nl = c * 64 + lane;
+    // relaxed atomic loads: nas_place filters against the working capacity
+    // while the commit stream publishes into it; padding nodes never fit
+    int fc = -1, fm = -1, fp = -1;
+    if (nl < nloc) {
+        int *cp = const_cast<int *>(cap) + n0 + nl;
+        fc = __hip_atomic_load(cp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fm = __hip_atomic_load(cp + N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fp = __hip_atomic_load(cp + 2 * (size_t)N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const int p = p0 + blockIdx.x * FIT_THREADS + tid;
-    const int q = min(p, Pp - 1);
-    const int ra = req[q], rb = req[Pp + q], rd = req[2 * Pp + q];
-    __syncthreads();
-    for (int c = c0; c < c1; ++c) {
-        const int *lc = &sc[0][(c - c0) * 64], *lm = &sc[1][(c - c0) * 64];
-        const int *lp = &sc[2][(c - c0) * 64];
-        unsigned w[2];
+    const int pend = min(p_end, pb0 + FIT_PODS);
+    for (int pb = pb0; pb < pend; pb += 64) {
+        unsigned lo = 0, hi = 0;
+        // lane i takes pod pb + i's word: three v_cmp of the pod's (uniform)
+        // requests against the lanes' capacities straight into SGPR lane
+        // masks, ANDed on the scalar unit, v_writelane into lane i
+        auto pod = [&](int i, int ra, int rb, int rd) {
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(ra <= fc) &
+                                         __builtin_amdgcn_ballot_w64(rb <= fm) &
+                                         __builtin_amdgcn_ballot_w64(rd <= fp);
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(lo) : "s"((unsigned)m), "i"(i));
+            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(hi) : "s"((unsigned)(m >> 32)), "i"(i));
+        };
+        if (pb + 64 <= Pp) {
+            // the group's requests through the scalar unit: wide s_loads of
+            // 64 consecutive ints per resource, issued together
+            const int *qa = req + pb, *qb = req + Pp + pb, *qd = req + 2 * (size_t)Pp + pb;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            unsigned acc = 0;
+            for (int k = 0; k < 4; ++k) {
+                const v16i_a4 a = *reinterpret_cast<const v16i_a4 *>(qa + 16 * k);
+                const v16i_a4 b = *reinterpret_cast<const v16i_a4 *>(qb + 16 * k);
+                const v16i_a4 d = *reinterpret_cast<const v16i_a4 *>(qd + 16 * k);
 #pragma unroll
-            for (int j4 = 7; j4 >= 0; --j4) {
-                const int o = h * 32 + j4 * 4;
-                const v4i fc = *reinterpret_cast<const v4i *>(lc + o);
-                const v4i fm = *reinterpret_cast<const v4i *>(lm + o);
-                const v4i fp = *reinterpret_cast<const v4i *>(lp + o);
-#pragma unroll
-                for (int j = 3; j >= 0; --j)
-                    acc = acc * 2u + ((ra <= fc[j] && rb <= fm[j] && rd <= fp[j]) ? 1u : 0u);
+                for (int i = 0; i < 16; ++i) pod(16 * k + i, a[i], b[i], d[i]);
             }
-            w[h] = acc;
+        } else {
+            // a window running past the padded rows (rescore views): one
+            // coalesced load per resource, broadcast with v_readlane
+            const int q = min(pb + lane, Pp - 1);
+            const int va = req[q], vb = req[Pp + q], vd = req[2 * Pp + q];
+#pragma unroll
+            for (int i = 0; i < 64; ++i)
+                pod(i, __builtin_amdgcn_readlane(va, i), __builtin_amdgcn_readlane(vb, i),
+                    __builtin_amdgcn_readlane(vd, i));
         }
-        if (p < p_end) mask[(size_t)c * Pp + p] = ((unsigned long long)w[1] << 32) | w[0];
+        if (pb + lane < pend) mask[(size_t)c * Pp + pb + lane] = ((unsigned long long)hi << 32) | lo;
     }
 }
 
@@ -93,8 +105,7 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
     (void)P;
     if (np <= 0) return hipSuccess;
     const int n_chunks = Mp / 64;
-    dim3 grid((np + FIT_THREADS - 1) / FIT_THREADS,
-              (n_chunks + FIT_CHUNKS - 1) / FIT_CHUNKS, batch);
+    dim3 grid((np + FIT_PODS - 1) / FIT_PODS, (n_chunks + FIT_WAVES - 1) / FIT_WAVES, batch);
     k_fit<<<grid, FIT_THREADS, 0, st>>>(cap, N, n0, nloc, n_chunks, req, Pp, p0,
                                         dyn ? dyn->hi : p0 + np,
                                         reinterpret_cast<unsigned long long *>(mask),
