@@ -26,12 +26,13 @@ typedef int v16i_a4 __attribute__((ext_vector_type(16), aligned(4)));
 
 constexpr int FIT_THREADS = 256;  // 4 waves = 4 node chunks per block
 constexpr int FIT_WAVES = FIT_THREADS / 64;
-constexpr int FIT_PODS = 512;     // pods per block (8 groups of 64)
+constexpr int FIT_GROUPS_MAX = 8;  // 64-pod groups per block (at most 512 pods)
 
 __global__ void __launch_bounds__(FIT_THREADS)
 k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
       const int *__restrict__ req, int Pp, int p0, int p_end, unsigned long long *__restrict__ mask,
-      const int *__restrict__ dyn_start, int dyn_win, const int *__restrict__ dyn_hi_ptr) {
+      const int *__restrict__ dyn_start, int dyn_win, const int *__restrict__ dyn_hi_ptr,
+      int block_pods) {
     if (dyn_start) {  // window [*dyn_start, +dyn_win) read from device memory (rescore slots)
         const int s = dyn_start[blockIdx.z * STATUS_INTS];
         if (s < 0) return;
@@ -39,7 +40,7 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
         if (dyn_hi_ptr) p_end = dyn_hi_ptr[blockIdx.z * STATUS_INTS];
         p_end = min(p_end, s + dyn_win);
     }
-    const int pb0 = p0 + (int)blockIdx.x * FIT_PODS;
+    const int pb0 = p0 + (int)blockIdx.x * block_pods;
     if (pb0 >= p_end) return;  // whole block (no barriers below)
     const int cb = blockIdx.z;  // cluster of a batched launch
     cap += (size_t)cb * 3 * N;
@@ -58,7 +59,7 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
         fm = __hip_atomic_load(cp + N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         fp = __hip_atomic_load(cp + 2 * (size_t)N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const int pend = min(p_end, pb0 + FIT_PODS);
+    const int pend = min(p_end, pb0 + block_pods);
     for (int pb = pb0; pb < pend; pb += 64) {
         unsigned lo = 0, hi = 0;
         // lane i takes pod pb + i's word: three v_cmp of the pod's (uniform)
@@ -105,12 +106,19 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
     (void)P;
     if (np <= 0) return hipSuccess;
     const int n_chunks = Mp / 64;
-    dim3 grid((np + FIT_PODS - 1) / FIT_PODS, (n_chunks + FIT_WAVES - 1) / FIT_WAVES, batch);
+    // pods per block: up to 512, fewer when the launch is small, so a rescore
+    // slot's few thousand pods still spread over ~2k blocks (each wave's pod
+    // groups run back to back: latency, not work, sets a small launch's time)
+    const int yb = (n_chunks + FIT_WAVES - 1) / FIT_WAVES;
+    const long long groups = ((long long)np + 63) / 64 * yb;
+    const int k = (int)std::max(1LL, std::min<long long>(FIT_GROUPS_MAX, groups / 2048));
+    const int block_pods = 64 * k;
+    dim3 grid((np + block_pods - 1) / block_pods, yb, batch);
     k_fit<<<grid, FIT_THREADS, 0, st>>>(cap, N, n0, nloc, n_chunks, req, Pp, p0,
                                         dyn ? dyn->hi : p0 + np,
                                         reinterpret_cast<unsigned long long *>(mask),
                                         dyn ? dyn->start : nullptr, dyn ? dyn->win : 0,
-                                        dyn ? dyn->hi_ptr : nullptr);
+                                        dyn ? dyn->hi_ptr : nullptr, block_pods);
     return hipGetLastError();
 }
 
