@@ -35,8 +35,8 @@ SEED = 0x4E4153
 # profiles/r01_final_prof_summary.json): FETCH_SIZE x 2 (gfx950 correction,
 # MI355X_MICROARCH.md) + WRITE_SIZE, for the default workload on one GPU only;
 # any other (kernel, dtype, nodes, pods, world) reports null.
-PMC_TRAFFIC = {("k_cost_topk", "i8", 10000, 100000, 1): 18592996992.0,
-               ("k_vote", "i8", 10000, 100000, 1): 48087100928.0}
+PMC_TRAFFIC = {("k_cost_topk", "i8", 10000, 100000, 1): 17999570176.0,
+               ("k_vote", "i8", 10000, 100000, 1): 48087265984.0}
 
 
 def parse():
