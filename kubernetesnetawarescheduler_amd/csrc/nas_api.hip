@@ -606,7 +606,7 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
         // the rest in equal chunks of at most `big` tiles
         const int n = (left + big - 1) / big;
         tiles = (left + n - 1) / n;
-    }
+    }  // (decreasing chunk sizes n, n-1, ..., 1 measured 7-10% slower at G = 4 / 8)
     return tiles * nas::COST_BN;
 }
 
