@@ -155,3 +155,30 @@ def test_rccl_world1_place_equals_oracle(P, N, crowd):
             assert (e.get_capacity() == wfree).all()
         if crowd:
             assert e.timings()["rescore_rounds"] > 0
+
+
+@pytest.mark.parametrize("G", [2, 8])
+def test_rehearsal_pass_is_well_formed(G, monkeypatch):
+    """bench.py --rehearse-world: rank 0 of a G-GPU pass on one GPU (shifted
+    copies stand in for the other ranks' lists, so placements are not the
+    oracle's).  The commit is real, so capacity is still conserved and every
+    placement is a node index that fitted."""
+    rng = np.random.default_rng(G)
+    P, N = 6000, 800
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=30, cap_scale=4.0)
+    monkeypatch.setenv("NAS_REHEARSE_WORLD", str(G))
+    with Engine(0) as e:
+        e.comm_init(Engine.comm_unique_id(), 0, 1)
+        monkeypatch.delenv("NAS_REHEARSE_WORLD")
+        e.upload_latency(L, "i8")
+        e.upload_capacity(free)
+        e.upload_pods(req)
+        e.upload_traffic(WA, "i8")
+        node, _, _ = e.place()
+        left = e.get_capacity()
+    assert ((node >= 0) & (node < N) | (node == -1)).all()
+    placed = node >= 0
+    used = np.zeros((N, 3), np.int64)
+    np.add.at(used, node[placed], req[placed].astype(np.int64))
+    assert (free.astype(np.int64) - used == left).all() and (left >= 0).all()
+    assert placed.sum() > P // 2
