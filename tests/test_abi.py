@@ -67,3 +67,11 @@ def test_null_context_is_an_argument_error():
     assert L.nas_score(None) == _lib.NAS_ERR_ARG
     assert L.nas_get_timings(None, None) == _lib.NAS_ERR_ARG
     assert L.nas_last_error(None) == b"null context"
+
+
+def test_missing_library_fails_loudly(monkeypatch):
+    # no CPU fallback: without the built libnas.so every entry point raises
+    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", os.path.join(ROOT, "no_such_dir", "libnas.so"))
+    with pytest.raises(_lib.NasError, match="not built"):
+        _lib.lib()
