@@ -32,11 +32,12 @@ PEAK_BF16_TFLOPS = 2516.6  # dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # HBM3E spec (MI355X_MICROARCH.md)
 SEED = 0x4E4153
 # HBM-side bytes per launch from rocprofv3 PMC passes (tools/prof_bench.sh ->
-# profiles/r01_final_prof_summary.json): FETCH_SIZE x 2 (gfx950 correction,
+# profiles/r01_s15_prof_summary.json; 16.8-18.6 GB across this round's
+# profiling boxes for k_cost_topk, as Infinity-Cache hits vary): FETCH_SIZE x 2 (gfx950 correction,
 # MI355X_MICROARCH.md) + WRITE_SIZE, for the default workload on one GPU only;
 # any other (kernel, dtype, nodes, pods, world) reports null.
-PMC_TRAFFIC = {("k_cost_topk", "i8", 10000, 100000, 1): 17999570176.0,
-               ("k_vote", "i8", 10000, 100000, 1): 48087265984.0}
+PMC_TRAFFIC = {("k_cost_topk", "i8", 10000, 100000, 1): 17630158848.0,
+               ("k_vote", "i8", 10000, 100000, 1): 48088230400.0}
 
 
 def parse():
