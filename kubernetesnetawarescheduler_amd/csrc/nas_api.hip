@@ -66,6 +66,18 @@ namespace {
 constexpr int RESCORE_PODS = 1024;  // pods per device-side rescore slot (multiple of COST_BN)
 constexpr int GATHER_PODS = 4096;   // dry pods rescored per gathered slot (gathered_slot)
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
+// ... except the second check: a walk still halted after a full batch is
+// usually nearly done (C2: 5 slots), and an idle slot's ~8 launches cost about
+// what one more host round trip does, so the second batch is one slot
+// (NAS_GATHER_SECOND overrides; C2 median 1.17 / 1.07 / 1.04 ms with a second
+// batch of 4 / 2 / 1, same placements)
+int gather_batch(int check) {
+    static const int second = [] {
+        const char *e = std::getenv("NAS_GATHER_SECOND");
+        return e ? std::max(1, std::atoi(e)) : 1;
+    }();
+    return check == 2 ? second : GATHER_SLOTS_PER_SYNC;
+}
 constexpr size_t HOST_OUT_OFFSET = 4096;  // pinned staging of nas_place results in host_status
 // Device-side rescore slots enqueued blindly behind a chunk's commit
 // (NAS_RESCORE_SLOTS overrides).  An idle gathered slot still costs ~0.1 ms
@@ -1287,7 +1299,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         // still halted after the pipeline: more gathered slots, checked in batches
         if (hs[0] >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
         if (++checks > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
-        for (int r = 0; r < GATHER_SLOTS_PER_SYNC; ++r)
+        for (int r = 0, n = gather_batch(checks); r < n; ++r)
             OK(gathered_slot(ctx, tm, st, ctx->comm, nullptr, P));
         OK(fetch());
         if (hs[0] < 0) {
