@@ -723,6 +723,7 @@ void nas_destroy(nas_ctx *ctx) {
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
+    if (ctx->ref_stage.p) (void)hipHostFree(ctx->ref_stage.p);
     destroy_comms(ctx);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
@@ -922,11 +923,25 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
         best_d = ctx->best.as<int32_t>();
         win_d = ctx->winners.as<int32_t>();
     }
-    HIPCK(hipMemcpyAsync(best_out, best_d, (size_t)P * 4, hipMemcpyDeviceToHost, ctx->stream));
+    // results come back through a pinned staging buffer (a copy into the
+    // caller's pageable memory is a blocking staged copy each: C1, 100 pods,
+    // spent most of its per-call time in the two of them)
+    const size_t stage_bytes = (size_t)P * 28;
+    if (ctx->ref_stage.bytes < stage_bytes) {
+        if (ctx->ref_stage.p) (void)hipHostFree(ctx->ref_stage.p);
+        ctx->ref_stage.p = nullptr;
+        ctx->ref_stage.bytes = 0;
+        HIPCK(hipHostMalloc(&ctx->ref_stage.p, stage_bytes, hipHostMallocDefault));
+        ctx->ref_stage.bytes = stage_bytes;
+    }
+    int32_t *stage = ctx->ref_stage.as<int32_t>();
+    HIPCK(hipMemcpyAsync(stage, best_d, (size_t)P * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (winners_out)
-        HIPCK(hipMemcpyAsync(winners_out, win_d, (size_t)P * 24, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCK(hipMemcpyAsync(stage + P, win_d, (size_t)P * 24, hipMemcpyDeviceToHost, ctx->stream));
     hipEvent_t c = tm.mark();
     HIPCK(hipStreamSynchronize(ctx->stream));
+    std::memcpy(best_out, stage, (size_t)P * 4);
+    if (winners_out) std::memcpy(winners_out, stage + P, (size_t)P * 24);
     tm.span(T_VOTE, a, b);
     tm.span(T_TOTAL, a, c);
     ctx->timings.vote_ms = tm.total(T_VOTE);

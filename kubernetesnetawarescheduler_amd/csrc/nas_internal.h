@@ -98,6 +98,7 @@ struct nas_ctx {
     nas::DevBuf g_gk, g_gb;                // gathered rescore exchange [world][R][KC] / [world][R]
     nas::DevBuf status;      // small device scratch for commit control
     nas::DevBuf host_status; // pinned
+    nas::DevBuf ref_stage;   // pinned: nas_score_reference results [P] best | [P][6] winners
     nas::DevBuf scratch;
     bool scored = false;        // a scoring pass filled cand_key
     bool synth_valid = false;   // inputs came from nas_synth_cluster(synth_seed)
