@@ -1226,6 +1226,10 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         chunks.push_back({lo, hi});
         lo = hi;
     }
+    // a one-chunk pass without a communicator has nothing to pipeline: its
+    // merge / commit / copies stay on the scoring stream, which saves the
+    // cross-stream event hops (~15-20 us each) that dominate a small pass
+    if (chunks.size() == 1 && !ctx->comm) sc = st;
     const bool split = merge_on_commit_stream();
     std::vector<hipEvent_t> scored(chunks.size());
     auto score_chunk = [&](size_t c) -> int {
