@@ -71,22 +71,17 @@ constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host ch
 // what one more host round trip does, so the second batch is one slot
 // (NAS_GATHER_SECOND overrides; C2 median 1.17 / 1.07 / 1.04 ms with a second
 // batch of 4 / 2 / 1, same placements)
-// The first batch is one slot too when the walk halted within its last
-// GATHER_PODS / 4 pods (C1: 12 pods rescored, 3 idle slots of 4 were most of
-// its nas_place time; C2 halts earlier, and a one-slot first batch cost it an
-// extra round trip: 1.04 -> 1.26 ms at a GATHER_PODS threshold).
-int gather_batch(int check, int remaining) {
+int gather_batch(int check) {
     static const int second = [] {
         const char *e = std::getenv("NAS_GATHER_SECOND");
         return e ? std::max(1, std::atoi(e)) : 1;
     }();
-    static const int first_max = [] {  // NAS_GATHER_FIRST_MAX overrides, for A/B runs
-        const char *e = std::getenv("NAS_GATHER_FIRST_MAX");
-        return e ? std::atoi(e) : GATHER_PODS / 4;
-    }();
-    if (check == 1 && remaining <= first_max) return 1;
     return check == 2 ? second : GATHER_SLOTS_PER_SYNC;
 }
+// (a one-slot FIRST batch for walks halting near their end helped a 12-pod
+// rescore, 0.39 -> 0.26 ms, but cost bench C1's 3-slot case two extra round
+// trips, 0.39 -> 0.52 ms: with a round trip ~2 idle slots, 4 then 1 is the
+// robust order)
 constexpr size_t HOST_OUT_OFFSET = 4096;  // pinned staging of nas_place results in host_status
 // Device-side rescore slots enqueued blindly behind a chunk's commit
 // (NAS_RESCORE_SLOTS overrides).  An idle gathered slot still costs ~0.1 ms
@@ -1229,7 +1224,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // a one-chunk pass without a communicator has nothing to pipeline: its
     // merge / commit / copies stay on the scoring stream, which saves the
     // cross-stream event hops (~15-20 us each) that dominate a small pass
-    if (chunks.size() == 1 && !ctx->comm) sc = st;
+    static const bool one_stream = [] {  // NAS_ONE_STREAM=0 turns this off, for A/B runs
+        const char *e = std::getenv("NAS_ONE_STREAM");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    if (one_stream && chunks.size() == 1 && !ctx->comm) sc = st;
     const bool split = merge_on_commit_stream();
     std::vector<hipEvent_t> scored(chunks.size());
     auto score_chunk = [&](size_t c) -> int {
@@ -1327,7 +1326,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         // still halted after the pipeline: more gathered slots, checked in batches
         if (hs[0] >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
         if (++checks > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
-        for (int r = 0, n = gather_batch(checks, P - hs[0]); r < n; ++r)
+        for (int r = 0, n = gather_batch(checks); r < n; ++r)
             OK(gathered_slot(ctx, tm, st, ctx->comm, nullptr, P));
         OK(fetch());
         if (hs[0] < 0) {

@@ -16,8 +16,8 @@ from kubernetesnetawarescheduler_amd import Engine  # noqa: E402
 
 def main():
     rng = np.random.default_rng(0x4E4153)
-    N = P = 10
-    P = 100
+    N, P = 10, 100
+    rng.permutation(N), rng.permutation(N + 1)  # bench.py draws the vote orders first
     L = rng.integers(1, 100, (N, N)).astype(np.int8)
     L = np.triu(L, 1) + np.triu(L, 1).T
     WA = np.zeros((P, N), np.int8)
