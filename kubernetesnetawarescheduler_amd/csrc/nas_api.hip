@@ -614,6 +614,14 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     const int mode = env_mode >= 0 ? env_mode : (big > 32 ? 2 : 0);
     const int left = (ctx->P - lo + nas::COST_BN - 1) / nas::COST_BN;  // pod tiles left
     int tiles = c == 0 ? 32 : big;
+    // a pass whose pods fit one big chunk (C2: 40 pod tiles on 4 node tiles)
+    // is one chunk: pipelining its short tail would save less than the
+    // cross-stream hops and launches it adds (NAS_CHUNK_WHOLE=0 turns this off)
+    static const bool whole = [] {
+        const char *e = std::getenv("NAS_CHUNK_WHOLE");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    if (whole && c == 0 && left <= big) tiles = left;
     if (mode == 0) {
         // a big last chunk is split in two so that the last is 32 tiles (unless
         // the first part would be a sliver of under 16)
