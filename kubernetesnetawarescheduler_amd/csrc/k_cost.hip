@@ -945,7 +945,7 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
         long long stride, long long bstride, int src_p0, int p0, int np,
         u64 *__restrict__ dst, u64 *__restrict__ dst_bound, int dst_p0,
         const int *__restrict__ dyn_start, int dyn_hi, int dyn_flags, long long dst_cs,
-        const int *__restrict__ dyn_hi_ptr) {
+        const int *__restrict__ dyn_hi_ptr, const int *__restrict__ dst_idx) {
     const int cb = blockIdx.y;  // cluster of a batched launch (dst_cs pods apart)
     keys += (size_t)cb * n_lists * stride;
     bounds += (size_t)cb * n_lists * bstride;
@@ -983,7 +983,10 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
         merge88(a, bb);
     }
     if (!live || s != 0) return;
-    const int p = p0 + i - dst_p0;
+    // dst_idx (gathered rescore view, one cluster): row r's lists go straight
+    // back to pod dst_idx[r]'s slots -- the scatter fused into the store
+    const int r = p0 + i - dst_p0;
+    const int p = dst_idx ? dst_idx[r] : r;
     store8(dst + (size_t)p * KC, a);
     dst_bound[p] = umin64(bound, a[7]);
 }
@@ -1066,14 +1069,16 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0, const Dyn *dyn,
-                        int dyn_flags, int batch, int64_t dst_cluster_pods) {
+                        int dyn_flags, int batch, int64_t dst_cluster_pods,
+                        const int32_t *dst_idx) {
     if (dyn) np = dyn->win;
     if (np <= 0) return hipSuccess;
+    if (dst_idx && batch != 1) return hipErrorInvalidValue;
     k_merge<<<dim3((int)(((int64_t)np * MERGE_LANES + 255) / 256), batch), 256, 0, st>>>(
         reinterpret_cast<const u64 *>(keys), reinterpret_cast<const u64 *>(bounds), n_lists, stride,
         bstride, src_p0, p0, np, reinterpret_cast<u64 *>(cand_key),
         reinterpret_cast<u64 *>(cand_bound), dst_p0, dyn ? dyn->start : nullptr, dyn ? dyn->hi : 0,
-        dyn_flags, (long long)dst_cluster_pods, dyn ? dyn->hi_ptr : nullptr);
+        dyn_flags, (long long)dst_cluster_pods, dyn ? dyn->hi_ptr : nullptr, dst_idx);
     return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@
 //   3. k_gather_pods: their traffic rows and requests are copied into a
 //      contiguous scratch "view" that the ordinary fit / cost / merge
 //      kernels (and the RCCL exchange) score like any pod range.
-//   4. k_scatter_lists: the fresh lists go back to the pods' list slots.
+//   4. k_merge's store puts the fresh lists back into the pods' list slots.
 // Lists computed against the capacity now stay valid for every later turn of
 // these pods (capacity only shrinks), so the walk resumes from s unchanged.
 #include "klist.h"
@@ -124,16 +124,6 @@ k_gather_pods(const int *__restrict__ idx, const int *__restrict__ count, const 
     }
 }
 
-__global__ void k_scatter_lists(const int *__restrict__ idx, const int *__restrict__ count,
-                                const u64 *__restrict__ key_v, const u64 *__restrict__ bound_v,
-                                u64 *__restrict__ key, u64 *__restrict__ bound) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = t / KC, j = t % KC;
-    if (i >= *count) return;
-    const int p = idx[i];
-    key[(size_t)p * KC + j] = key_v[(size_t)i * KC + j];
-    if (j == 0) bound[p] = bound_v[i];
-}
 
 }  // namespace
 
@@ -166,14 +156,5 @@ hipError_t launch_gather_pods(hipStream_t st, const int32_t *idx, const int32_t 
     return hipGetLastError();
 }
 
-hipError_t launch_scatter_lists(hipStream_t st, const int32_t *idx, const int32_t *count, int Rv,
-                                const uint64_t *key_v, const uint64_t *bound_v, uint64_t *key,
-                                uint64_t *bound) {
-    const int total = Rv * KC;
-    k_scatter_lists<<<(total + 255) / 256, 256, 0, st>>>(
-        idx, count, reinterpret_cast<const u64 *>(key_v), reinterpret_cast<const u64 *>(bound_v),
-        reinterpret_cast<u64 *>(key), reinterpret_cast<u64 *>(bound));
-    return hipGetLastError();
-}
 
 }  // namespace nas

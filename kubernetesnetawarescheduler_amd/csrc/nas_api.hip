@@ -356,19 +356,23 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t
                                 ctx->Nloc0, &dyn));
     hipEvent_t e3 = tm.mark(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
+    // the last merge writes the fresh lists straight into the pods' own list
+    // slots (idx); with an exchange, the local merge first fills the view
+    const bool xch = exchanging(ctx);
+    auto *ck = ctx->cand_key.as<uint64_t>();
+    auto *cbnd = ctx->cand_bound.as<uint64_t>();
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
-                            (int64_t)R * KC, R, 0, 0, 0, gk, gb, 0, &dyn, 0));
-    if (exchanging(ctx)) {
+                            (int64_t)R * KC, R, 0, 0, 0, xch ? gk : ck, xch ? gb : cbnd, 0, &dyn,
+                            0, 1, 0, xch ? nullptr : idx));
+    if (xch) {
         OK(nas::ensure(ctx, ctx->g_gk, (size_t)ctx->world * R * KC * 8));
         OK(nas::ensure(ctx, ctx->g_gb, (size_t)ctx->world * R * 8));
         auto *xk = ctx->g_gk.as<uint64_t>();
         auto *xb = ctx->g_gb.as<uint64_t>();
         OK(exchange(ctx, cm, st, gk, gb, (size_t)R, xk, xb));
-        HIPCK(nas::launch_merge(st, xk, xb, ctx->world, (int64_t)R * KC, R, 0, 0, 0, gk, gb, 0,
-                                &dyn, 0));
+        HIPCK(nas::launch_merge(st, xk, xb, ctx->world, (int64_t)R * KC, R, 0, 0, 0, ck, cbnd, 0,
+                                &dyn, 0, 1, 0, idx));
     }
-    HIPCK(nas::launch_scatter_lists(st, idx, ctl + 1, R, gk, gb, ctx->cand_key.as<uint64_t>(),
-                                    ctx->cand_bound.as<uint64_t>()));
     hipEvent_t e4 = tm.mark(st);
     HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), ctx->Pp, -1, hi, ctx->cap.as<int32_t>(),

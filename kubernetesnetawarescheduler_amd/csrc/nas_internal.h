@@ -178,7 +178,7 @@ hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bo
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,
                         const Dyn *dyn = nullptr, int dyn_flags = 0, int batch = 1,
-                        int64_t dst_cluster_pods = 0);
+                        int64_t dst_cluster_pods = 0, const int32_t *dst_idx = nullptr);
 // the commit keeps the working capacity in LDS (and publishes only final
 // values, at the end of each launch) for clusters of up to this many nodes
 bool commit_in_lds(int N);
@@ -199,9 +199,6 @@ hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t
 hipError_t launch_gather_pods(hipStream_t st, const int32_t *idx, const int32_t *count,
                               const void *WA, size_t row_bytes, const int32_t *req, int Pp, int Rv,
                               void *WA_v, int32_t *req_v);
-hipError_t launch_scatter_lists(hipStream_t st, const int32_t *idx, const int32_t *count, int Rv,
-                                const uint64_t *key_v, const uint64_t *bound_v, uint64_t *key,
-                                uint64_t *bound);
 
 // start of a nas_place pass: status[0] = -1 (halt), status[1 .. 2*STATUS_INTS)
 // = 0; cap_snap[0, n) = cap[0, n) when cap_snap is non-null
