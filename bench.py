@@ -87,13 +87,18 @@ class Dist:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
             self.dist = dist
-        torch.cuda.set_device(self.local)
+        # (no GPU: the rank logic alone, as the CPU gloo tests run it)
+        self.gpu = torch.cuda.is_available()
+        if self.gpu:
+            torch.cuda.set_device(self.local)
 
     def barrier_sync(self):
-        self.torch.cuda.synchronize()
+        if self.gpu:
+            self.torch.cuda.synchronize()
         if self.world > 1:
             self.dist.barrier()
-        self.torch.cuda.synchronize()
+        if self.gpu:
+            self.torch.cuda.synchronize()
 
     def max(self, x):
         if self.world == 1:
@@ -125,11 +130,10 @@ def bench_place(args, d, eng):
     N, P = args.nodes, args.pods
     if args.rehearse_world > 1:
         assert d.world == 1, "--rehearse-world runs on one GPU"
-        os.environ["NAS_REHEARSE_WORLD"] = str(args.rehearse_world)
+        eng.set_option("REHEARSE_WORLD", args.rehearse_world)  # diagnostic option
     if d.world > 1 or args.rccl_world1 or args.rehearse_world > 1:
         uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
         eng.comm_init(uid, d.rank, d.world)
-        os.environ.pop("NAS_REHEARSE_WORLD", None)
     eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
     if args.rehearse_world > 1:
         # the stand-in lists repeat this rank's few best nodes G times, so
@@ -158,9 +162,9 @@ def bench_place(args, d, eng):
         acc[k] = 0.0
     # timed steps record only the events the pass synchronises on; the
     # per-stage device times come from separate steps with stage timings on
-    os.environ["NAS_STAGE_TIMINGS"] = "0"
+    eng.set_option("STAGE_TIMINGS", 0)
     elapsed = time_steps(d, step, args.steps, 0)
-    os.environ.pop("NAS_STAGE_TIMINGS")
+    eng.set_option("STAGE_TIMINGS", 1)
     per = {k: v / args.steps for k, v in acc.items()}
     for k in keys:
         acc[k] = 0.0

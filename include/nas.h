@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define NAS_ABI_VERSION 1
+#define NAS_ABI_VERSION 2
 
 /* status codes */
 #define NAS_OK 0
@@ -53,6 +53,8 @@ extern "C" {
 /* element types of the traffic (WA) and latency (L) matrices */
 #define NAS_DT_I8 1   /* int8, int32 accumulation: exact integer scores */
 #define NAS_DT_BF16 2 /* bf16 bits (uint16), fp32 accumulation */
+#define NAS_DT_I32 3  /* traffic only, with NAS_DT_I8 latency: int32 traffic, exact integer
+                       * scores (see nas_upload_traffic_dense) */
 
 /* winner slots returned by nas_score_reference (order of scheduler.go:360-365) */
 #define NAS_W_CPU 0
@@ -75,6 +77,29 @@ typedef struct nas_config {
     int32_t reserved0;
     int32_t reserved1;
 } nas_config;
+
+/* Per-context options (nas_set_option); every option has a production
+ * default, and nothing is read from the environment. */
+#define NAS_OPT_STAGE_TIMINGS 1  /* 1 (default): per-stage HIP events (nas_get_timings
+                                  * fit/cost/merge/commit); 0: only the events a call
+                                  * synchronises on (total_ms stays valid) */
+#define NAS_OPT_COMM_TIMEOUT_MS 2 /* deadline of every wait of a call that issued RCCL
+                                   * collectives, in ms (default 120000; 0 = no deadline).
+                                   * On expiry the communicators are aborted
+                                   * (ncclCommAbort), the call returns NAS_ERR_COMM and the
+                                   * context is poisoned: every later call except
+                                   * nas_last_error / nas_destroy returns NAS_ERR_COMM */
+#define NAS_OPT_REHEARSE_WORLD 3 /* DIAGNOSTIC, default 0.  G > 1, set before nas_comm_init
+                                  * with world 1: the context takes rank 0's shard geometry
+                                  * of a G-rank node shard and stands the other ranks' lists
+                                  * in with shifted copies of its own -- times one rank of a
+                                  * G-GPU pass on one GPU.  Placements are NOT meaningful. */
+#define NAS_OPT_INJECT_STALL_MS 4 /* TEST ONLY, default 0: the next call with a
+                                   * communicator enqueues a device-side delay of this many
+                                   * ms behind its collectives, on the stream it waits on
+                                   * last (exercises NAS_OPT_COMM_TIMEOUT_MS); cleared when
+                                   * used */
+int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value);
 
 /* per-stage device times of the last nas_place / nas_score_reference call,
  * measured with HIP events on the context's stream */
@@ -187,7 +212,9 @@ int nas_vote_merge(nas_ctx *ctx, const nas_vote_partial *parts, int32_t n_parts,
  */
 
 /* Dense latency matrix L[m * n + j] = latency from node m to node j,
- * uploaded once (dtype NAS_DT_I8 or NAS_DT_BF16). */
+ * uploaded once (dtype NAS_DT_I8 or NAS_DT_BF16).  Integer scores are exact
+ * int32: nas_place / nas_score return NAS_ERR_UNSUPPORTED when some pod's
+ * sum_m |WA[p,m]| * max|L| exceeds INT32_MAX. */
 int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n);
 
 /* Free capacity per node; also resets the working capacity nas_place uses. */
@@ -206,15 +233,19 @@ int nas_upload_pods(nas_ctx *ctx, const int32_t *req_cpu_milli, const int32_t *r
                     const int32_t *req_pods, int32_t P);
 
 /* Traffic of each pending pod to each node, WA[p * n + m] = sum of
- * W[p,q] over already-bound peers q with node(q) == m (dense, same dtype as L). */
+ * W[p,q] over already-bound peers q with node(q) == m (dense).  dtype: the
+ * latency's (NAS_DT_I8 / NAS_DT_BF16), or NAS_DT_I32 with NAS_DT_I8 latency --
+ * the cost stays the exact sum_m WA[p,m] * L[m,n] for any int32 traffic (the
+ * engine keeps an int8 plane for the MFMA and adds the few entries outside
+ * [-128, 127] exactly in the contraction's epilogue). */
 int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_t P, int32_t n);
 
 /* Same from a sparse pod-communication graph: for pod p the peers are
  * peer_node[row_ptr[p] .. row_ptr[p+1]) (node of an already-bound peer, or
- * -1 for an unbound peer, which is skipped) with weights weight[...]
- * (int8 for NAS_DT_I8 -- summed in int32, saturated to [-128, 127] -- or bf16
- * bits for NAS_DT_BF16, summed in fp32 and rounded once).  Aggregated on the
- * device into the dense WA. */
+ * -1 for an unbound peer, which is skipped) with weights weight[...]:
+ * int8 (NAS_DT_I8) or int32 (NAS_DT_I32) with int8 latency -- summed exactly
+ * (no saturation; an aggregate outside int32 is NAS_ERR_UNSUPPORTED) -- or
+ * bf16 bits (NAS_DT_BF16), summed in fp32 on the device and rounded once. */
 int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *peer_node,
                            const void *weight, int32_t dtype, int32_t P, int32_t n,
                            int64_t nnz);
@@ -333,7 +364,9 @@ int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, i
 int nas_synth_batch(nas_ctx *ctx, uint64_t seed, int32_t n_clusters, int32_t n_nodes, int32_t P,
                     int32_t dtype, int32_t peers);
 /* Read back rows of the device-resident inputs (for sampled oracle checks):
- * WA rows [p0, p0+np), the full L, capacity and requests (cluster 0 of a batch). */
+ * WA rows [p0, p0+np) -- int32 [np][n] exact traffic for int8 scoring, bf16
+ * bits [np][n] otherwise --, the full L, capacity and requests (cluster 0 of a
+ * batch). */
 int nas_read_inputs(nas_ctx *ctx, int32_t p0, int32_t np, void *WA_rows, void *L,
                     int32_t *cap_cpu, int32_t *cap_mem, int32_t *cap_pods, int32_t *req_cpu,
                     int32_t *req_mem, int32_t *req_pods);

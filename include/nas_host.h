@@ -114,7 +114,7 @@ typedef struct nas_host_pod {
     int32_t cpu_milli, mem_kib;       /* requests (network-aware path) */
     int32_t n_peers;
     const char *const *peers;         /* "namespace/name" of each peer pod */
-    const int32_t *peer_weight;       /* traffic to each peer (int8 range) */
+    const int32_t *peer_weight;       /* traffic to each peer (any int32; exact sums) */
 } nas_host_pod;
 
 /* informer AddFunc (:166-176): 1 queued, 0 filtered out (bound, or another

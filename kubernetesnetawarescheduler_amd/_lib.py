@@ -22,6 +22,11 @@ NAS_NONE = -2
 NAS_EMPTY = -1
 NAS_DT_I8 = 1
 NAS_DT_BF16 = 2
+NAS_DT_I32 = 3  # traffic only (int8 latency): exact int32 traffic
+NAS_OPT_STAGE_TIMINGS = 1
+NAS_OPT_COMM_TIMEOUT_MS = 2
+NAS_OPT_REHEARSE_WORLD = 3
+NAS_OPT_INJECT_STALL_MS = 4
 K_CANDIDATES = 8
 VOTE_NOPOS = 0x7FFFFFFF
 # include/nas.h nas_vote_partial: six (value, pos1, reserved) extrema, NAS_VP_* order
@@ -69,6 +74,7 @@ SIGNATURES = {
     "nas_destroy": (None, [_CTX]),
     "nas_last_error": (_c.c_char_p, [_CTX]),
     "nas_get_timings": (_I, [_CTX, _c.POINTER(NasTimings)]),
+    "nas_set_option": (_I, [_CTX, _I, _c.c_int64]),
     "nas_upload_snapshot": (_I, [_CTX, _V, _V, _V, _V, _V, _V, _I, _I]),
     "nas_upload_orders": (_I, [_CTX, _V, _V, _I]),
     "nas_score_reference": (_I, [_CTX, _V, _V, _V, _I, _V, _V]),

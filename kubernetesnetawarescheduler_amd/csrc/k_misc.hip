@@ -3,6 +3,8 @@
 // into HBM (benchmarks; SURVEY.md §8(d) workload shapes).
 #include "nas_internal.h"
 
+#include <algorithm>
+
 namespace nas {
 namespace {
 
@@ -27,27 +29,10 @@ __global__ void k_transpose(const T *__restrict__ L, int N, int n0, int nloc, in
 }
 
 // --------------------------------------------------------- CSR aggregation
-// WA[p][m] = sum of weights of p's peers bound to node m (row zeroed before).
-// One thread per pod; peers per pod are few, so the O(nnz_p^2) dedupe walk is
-// cheap and needs no atomics.
-__global__ void k_csr_i8(const int *__restrict__ row_ptr, const int *__restrict__ peer,
-                         const signed char *__restrict__ w, int P, int N, int Kp,
-                         signed char *__restrict__ WA) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P) return;
-    const int b = row_ptr[p], e = row_ptr[p + 1];
-    for (int x = b; x < e; ++x) {
-        const int m = peer[x];
-        if (m < 0 || m >= N) continue;
-        bool seen = false;
-        for (int y = b; y < x && !seen; ++y) seen = peer[y] == m;
-        if (seen) continue;
-        int s = 0;
-        for (int y = x; y < e; ++y) s += peer[y] == m ? (int)w[y] : 0;
-        WA[(size_t)p * Kp + m] = (signed char)max(-128, min(127, s));
-    }
-}
-
+// bf16 traffic: WA[p][m] = sum of weights of p's peers bound to node m (row
+// zeroed before), in fp32, rounded once.  One thread per pod; peers per pod
+// are few, so the O(nnz_p^2) dedupe walk is cheap and needs no atomics.  (The
+// int8 path aggregates exactly on the host: nas_upload_traffic_csr.)
 __global__ void k_csr_bf16(const int *__restrict__ row_ptr, const int *__restrict__ peer,
                            const unsigned short *__restrict__ w, int P, int N, int Kp,
                            unsigned short *__restrict__ WA) {
@@ -151,16 +136,9 @@ template <>
 __device__ __forceinline__ signed char from_int<signed char>(int v) { return (signed char)v; }
 template <>
 __device__ __forceinline__ unsigned short from_int<unsigned short>(int v) {
-    return (unsigned short)(__float_as_uint((float)v) >> 16);  // exact for |v| <= 256
-}
-
-template <typename T>
-__device__ __forceinline__ int to_int(T v);
-template <>
-__device__ __forceinline__ int to_int<signed char>(signed char v) { return v; }
-template <>
-__device__ __forceinline__ int to_int<unsigned short>(unsigned short v) {
-    return (int)__uint_as_float((unsigned)v << 16);
+    // round to nearest even (exact for |v| <= 256)
+    const unsigned u = __float_as_uint((float)v);
+    return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
 // dense background traffic 0..2 to every node (every pod talks a little to
@@ -169,22 +147,22 @@ __device__ __forceinline__ int to_int<unsigned short>(unsigned short v) {
 // peer traffic (at 50k nodes a full background would be ~50 GB per pod
 // against ~0.6 GB to its peers, and every pod would rank nodes alike).
 constexpr int BG_NODES = 10000;
+// background traffic of pod p < P to node m < N (element t = p * Kp + m)
+__device__ __forceinline__ int bg_value(unsigned long long seed, int N, long long t) {
+    const unsigned long long h = mix64(seed ^ ((unsigned long long)t * 0x9e3779b97f4a7c15ull));
+    // past BG_NODES nodes each entry is kept with probability BG_NODES / N: a
+    // pod's total background volume stays that of a BG_NODES-node cluster
+    // instead of growing with N
+    const bool keep = N <= BG_NODES || (int)((h >> 32) % (unsigned)N) < BG_NODES;
+    return keep ? (int)(h % 3) : 0;
+}
 template <typename T>
 __global__ void k_synth_bg(unsigned long long seed, int N, int P, int Kp, long long total,
                            T *__restrict__ WA) {
     for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
          t += (long long)gridDim.x * blockDim.x) {
         const int p = (int)(t / Kp), m = (int)(t - (long long)p * Kp);
-        int v = 0;
-        if (p < P && m < N) {
-            const unsigned long long h = mix64(seed ^ ((unsigned long long)t * 0x9e3779b97f4a7c15ull));
-            // past BG_NODES nodes each entry is kept with probability
-            // BG_NODES / N: a pod's total background volume stays that of a
-            // BG_NODES-node cluster instead of growing with N
-            const bool keep = N <= BG_NODES || (int)((h >> 32) % (unsigned)N) < BG_NODES;
-            v = keep ? (int)(h % 3) : 0;
-        }
-        WA[t] = from_int<T>(v);
+        WA[t] = from_int<T>(p < P && m < N ? bg_value(seed, N, t) : 0);
     }
 }
 
@@ -209,18 +187,13 @@ __global__ void k_synth_lfull(unsigned long long seed, int N, T *__restrict__ L)
     }
 }
 
-// one thread per pod: heavy peers in the home rack (all but 2) and in the
-// zone, added on top of the background
-template <typename T>
-__global__ void k_synth_pods(unsigned long long seed, int N, int P, int peers, int Kp, int Pp,
-                             T *__restrict__ WA, int *__restrict__ req) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= Pp) return;
-    if (p >= P) { req[p] = 0; req[Pp + p] = 0; req[2 * Pp + p] = 0; return; }
+// The heavy peers of pod p: nodes[j], wts[j] for j < min(peers, 16) -- in the
+// home rack (all but 2) and in the zone.
+__device__ __forceinline__ int synth_peers(unsigned long long seed, int N, int p, int peers,
+                                           int (&nodes)[16], int (&wts)[16]) {
     const int n_racks = (N + 31) / 32;
     const unsigned long long hp = hsh(seed, p, 0, 11);
     const int rack = (int)(hp % n_racks);
-    int nodes[16], wts[16];
     const int np = min(peers, 16);
     for (int j = 0; j < np; ++j) {
         const unsigned long long h = hsh(seed, p, j + 1, 12);
@@ -235,13 +208,29 @@ __global__ void k_synth_pods(unsigned long long seed, int N, int P, int peers, i
         nodes[j] = min(node, N - 1);
         wts[j] = 16 + (int)((h >> 40) % 112);
     }
+    return np;
+}
+
+// one thread per pod: the heavy peers added on top of the background (exact
+// sums; the int8 plane holds them clamped to [-128, 127], the excess goes to
+// the overflow lists of launch_synth_overflow), and the pod's requests
+template <typename T>
+__global__ void k_synth_pods(unsigned long long seed, int N, int P, int peers, int Kp, int Pp,
+                             T *__restrict__ WA, int *__restrict__ req) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= Pp) return;
+    if (p >= P) { req[p] = 0; req[Pp + p] = 0; req[2 * Pp + p] = 0; return; }
+    int nodes[16], wts[16];
+    const int np = synth_peers(seed, N, p, peers, nodes, wts);
     for (int j = 0; j < np; ++j) {
         bool seen = false;
         for (int y = 0; y < j; ++y) seen |= nodes[y] == nodes[j];
         if (seen) continue;
-        int s = to_int<T>(WA[(size_t)p * Kp + nodes[j]]);  // background
+        const long long t = (long long)p * Kp + nodes[j];
+        int s = bg_value(seed, N, t);
         for (int y = j; y < np; ++y) s += nodes[y] == nodes[j] ? wts[y] : 0;
-        WA[(size_t)p * Kp + nodes[j]] = from_int<T>(min(s, 127));
+        if constexpr (sizeof(T) == 1) s = min(s, 127);  // the plane; the rest is overflow
+        WA[t] = from_int<T>(s);
     }
     const unsigned long long hr = hsh(seed, p, 0, 13);
     const double lc0 = -3.6716, lc1 = -0.2695;  // log10 of 0.000213, 0.5376 cores
@@ -251,6 +240,33 @@ __global__ void k_synth_pods(unsigned long long seed, int N, int P, int peers, i
     req[p] = max(1, (int)ceil(cores * 1000.0));
     req[Pp + p] = (int)ceil(bytes / 1024.0);
     req[2 * Pp + p] = 1;
+}
+
+// int8 overflow lists of the synthetic traffic (see launch_synth_overflow)
+__global__ void k_synth_ovf(unsigned long long seed, int N, int P, int peers, int Kp, int pass,
+                            int *__restrict__ cnt, const int *__restrict__ ptr,
+                            int *__restrict__ om, int *__restrict__ oe) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    int nodes[16], wts[16];
+    const int np = synth_peers(seed, N, p, peers, nodes, wts);
+    int c = 0;
+    const int base = pass ? ptr[p] : 0;
+    for (int j = 0; j < np; ++j) {
+        bool seen = false;
+        for (int y = 0; y < j; ++y) seen |= nodes[y] == nodes[j];
+        if (seen) continue;
+        int s = bg_value(seed, N, (long long)p * Kp + nodes[j]);
+        for (int y = j; y < np; ++y) s += nodes[y] == nodes[j] ? wts[y] : 0;
+        if (s > 127) {
+            if (pass) {
+                om[base + c] = nodes[j];
+                oe[base + c] = s - 127;
+            }
+            ++c;
+        }
+    }
+    if (!pass) cnt[p] = c;
 }
 
 __global__ void k_synth_cap(unsigned long long seed, int N, int *__restrict__ cap) {
@@ -265,6 +281,74 @@ __global__ void k_synth_cap(unsigned long long seed, int N, int *__restrict__ ca
 inline int grid_for(long long total, int threads) {
     long long g = (total + threads - 1) / threads;
     return (int)(g < 65536 ? (g > 0 ? g : 1) : 65536);
+}
+
+// WA[pod[i]][node[i]] = val[i]
+__global__ void k_plane_scatter(const int *__restrict__ pod, const int *__restrict__ node,
+                                const signed char *__restrict__ val, long long n, int Kp,
+                                signed char *__restrict__ WA) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        WA[(size_t)pod[i] * Kp + node[i]] = val[i];
+}
+
+// Lr[m][i] = Lt[i][m], m < N, i < Mp: 64 x 64 tiles through LDS
+__global__ void k_make_lr(const signed char *__restrict__ Lt, int N, int Mp, int Kp,
+                          signed char *__restrict__ Lr) {
+    __shared__ signed char tile[64][65];
+    const int i0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int r = ty; r < 64; r += 4) {
+        const int i = i0 + r, m = m0 + tx;
+        tile[r][tx] = (i < Mp && m < Kp) ? Lt[(size_t)i * Kp + m] : 0;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+        const int m = m0 + r, i = i0 + tx;
+        if (m < N && i < Mp) Lr[(size_t)m * Mp + i] = tile[tx][r];
+    }
+}
+
+// one wave per row: sum_k |plane[r][k]|, corrected by the row's overflow
+// entries (|plane + e| - |plane|), max over rows into *out
+__global__ void k_row_abs_max(const signed char *__restrict__ WA, long long rows, int Kp,
+                              const int *__restrict__ optr, const int *__restrict__ om,
+                              const int *__restrict__ oe, unsigned long long *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const long long w0 = (blockIdx.x * (long long)blockDim.x + threadIdx.x) >> 6;
+    const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+    for (long long r = w0; r < rows; r += nw) {
+        const signed char *row = WA + (size_t)r * Kp;
+        long long s = 0;
+        for (int k = lane * 4; k < Kp; k += 256) {
+            const int v = *reinterpret_cast<const int *>(row + k);
+            s += abs((signed char)(v & 0xff)) + abs((signed char)((v >> 8) & 0xff)) +
+                 abs((signed char)((v >> 16) & 0xff)) + abs((signed char)(v >> 24));
+        }
+        if (optr)
+            for (int j = optr[r] + lane; j < optr[r + 1]; j += 64) {
+                const long long pl = row[om[j]];
+                s += llabs(pl + oe[j]) - llabs(pl);
+            }
+        for (int o = 32; o; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0) atomicMax(out, (unsigned long long)s);
+    }
+}
+
+__global__ void k_abs_max_i8(const signed char *__restrict__ a, long long n,
+                             unsigned *__restrict__ out) {
+    unsigned m = 0;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        m = max(m, (unsigned)abs((int)a[i]));
+    for (int o = 32; o; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+// NAS_OPT_INJECT_STALL_MS: one lane spins on the 100 MHz real-time counter
+__global__ void k_stall(unsigned long long ticks) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
 __global__ void k_pass_init(int *__restrict__ status, const int *__restrict__ cap,
@@ -312,16 +396,45 @@ hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int 
     return hipGetLastError();
 }
 
-hipError_t launch_csr_aggregate(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
-                                const void *w, int dtype, int P, int N, int Kp, void *WA) {
+hipError_t launch_csr_aggregate_bf16(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
+                                     const uint16_t *w, int P, int N, int Kp, uint16_t *WA) {
     if (P <= 0) return hipSuccess;
-    if (dtype == NAS_DT_I8)
-        k_csr_i8<<<(P + 255) / 256, 256, 0, st>>>(row_ptr, peer, static_cast<const signed char *>(w),
-                                                  P, N, Kp, static_cast<signed char *>(WA));
-    else
-        k_csr_bf16<<<(P + 255) / 256, 256, 0, st>>>(row_ptr, peer,
-                                                    static_cast<const unsigned short *>(w), P, N,
-                                                    Kp, static_cast<unsigned short *>(WA));
+    k_csr_bf16<<<(P + 255) / 256, 256, 0, st>>>(row_ptr, peer, w, P, N, Kp, WA);
+    return hipGetLastError();
+}
+
+hipError_t launch_plane_scatter(hipStream_t st, const int32_t *pod, const int32_t *node,
+                                const signed char *val, int64_t n, int Kp, signed char *WA) {
+    if (n <= 0) return hipSuccess;
+    k_plane_scatter<<<grid_for(n, 256), 256, 0, st>>>(pod, node, val, (long long)n, Kp, WA);
+    return hipGetLastError();
+}
+
+hipError_t launch_make_lr(hipStream_t st, const signed char *Lt, int N, int Mp, int Kp,
+                          signed char *Lr) {
+    k_make_lr<<<dim3((Mp + 63) / 64, (N + 63) / 64), 256, 0, st>>>(Lt, N, Mp, Kp, Lr);
+    return hipGetLastError();
+}
+
+hipError_t launch_row_abs_max(hipStream_t st, const signed char *WA, int64_t rows, int Kp,
+                              const int32_t *ovf_ptr, const int32_t *ovf_m, const int32_t *ovf_e,
+                              unsigned long long *out) {
+    if (rows <= 0) return hipSuccess;
+    if (Kp % 4) return hipErrorInvalidValue;
+    k_row_abs_max<<<grid_for(rows * 64, 256), 256, 0, st>>>(WA, (long long)rows, Kp, ovf_ptr,
+                                                            ovf_m, ovf_e, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_abs_max_i8(hipStream_t st, const signed char *a, int64_t n, unsigned *out) {
+    if (n <= 0) return hipSuccess;
+    k_abs_max_i8<<<std::min(grid_for(n, 256), 4096), 256, 0, st>>>(a, (long long)n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_stall(hipStream_t st, int64_t ms) {
+    if (ms <= 0) return hipSuccess;
+    k_stall<<<1, 64, 0, st>>>((unsigned long long)ms * 100000ull);
     return hipGetLastError();
 }
 
@@ -379,6 +492,15 @@ hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+hipError_t launch_synth_overflow(hipStream_t st, uint64_t seed, int N, int P, int peers, int Kp,
+                                 int pass, const signed char *WA, int32_t *ovf_cnt,
+                                 const int32_t *ovf_ptr, int32_t *ovf_m, int32_t *ovf_e) {
+    (void)WA;  // the aggregates are recomputed from the seed
+    k_synth_ovf<<<(P + 255) / 256, 256, 0, st>>>(seed, N, P, peers, Kp, pass, ovf_cnt, ovf_ptr,
+                                                  ovf_m, ovf_e);
+    return hipGetLastError();
 }
 
 }  // namespace nas

@@ -8,9 +8,9 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "nas_internal.h"
@@ -68,33 +68,28 @@ constexpr int GATHER_PODS = 4096;   // dry pods rescored per gathered slot (gath
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
 // ... except the second check: a walk still halted after a full batch is
 // usually nearly done (C2: 5 slots), and an idle slot's ~8 launches cost about
-// what one more host round trip does, so the second batch is one slot
-// (NAS_GATHER_SECOND overrides; C2 median 1.17 / 1.07 / 1.04 ms with a second
-// batch of 4 / 2 / 1, same placements)
-int gather_batch(int check) {
-    static const int second = [] {
-        const char *e = std::getenv("NAS_GATHER_SECOND");
-        return e ? std::max(1, std::atoi(e)) : 1;
-    }();
-    return check == 2 ? second : GATHER_SLOTS_PER_SYNC;
-}
+// what one more host round trip does, so the second batch is one slot (C2
+// median 1.17 / 1.07 / 1.04 ms with a second batch of 4 / 2 / 1, same
+// placements)
+int gather_batch(int check) { return check == 2 ? 1 : GATHER_SLOTS_PER_SYNC; }
 // (a one-slot FIRST batch for walks halting near their end helped a 12-pod
 // rescore, 0.39 -> 0.26 ms, but cost bench C1's 3-slot case two extra round
 // trips, 0.39 -> 0.52 ms: with a round trip ~2 idle slots, 4 then 1 is the
 // robust order)
 constexpr size_t HOST_OUT_OFFSET = 4096;  // pinned staging of nas_place results in host_status
-// Device-side rescore slots enqueued blindly behind a chunk's commit
-// (NAS_RESCORE_SLOTS overrides).  An idle gathered slot still costs ~0.1 ms
-// of launches (C3, measured), more than the host round trip a stop costs once
-// the pipeline is done -- the results fetch brings the halt word back with
-// the placements -- and scoring against the live capacity makes stops rare:
-// by default slots run only for a walk known to have halted.
-constexpr int RESCORE_SLOTS = 0;
-constexpr int RESCORE_SLOTS_LAST = 0;
+// Rescore slots run only for a walk known to have halted (after the
+// pipeline): an idle gathered slot still costs ~0.1 ms of launches (C3,
+// measured), more than the host round trip a stop costs once the pipeline is
+// done -- the results fetch brings the halt word back with the placements --
+// and scoring against the live capacity makes stops rare.
 
 int bind(nas_ctx *ctx) {
     if (!ctx) return NAS_ERR_ARG;
     ctx->err.clear();
+    if (ctx->poisoned)
+        return nas::fail(ctx, NAS_ERR_COMM,
+                         "context poisoned: a collective missed its deadline and the "
+                         "communicators were aborted (destroy the context)");
     HIPCK(hipSetDevice(ctx->device));
     return NAS_OK;
 }
@@ -124,13 +119,12 @@ struct Timer {
         if (e) (void)hipEventRecord(e, st ? st : ctx->stream);
         return e;
     }
-    // a timing-only mark: none when stage timings are off (NAS_STAGE_TIMINGS=0,
-    // read per call), so the pass records only the events it synchronises on
-    bool fine_on = [] {
-        const char *e = std::getenv("NAS_STAGE_TIMINGS");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    hipEvent_t fine(hipStream_t st = nullptr) { return fine_on ? mark(st) : nullptr; }
+    // a timing-only mark: none when stage timings are off
+    // (NAS_OPT_STAGE_TIMINGS = 0), so the pass records only the events it
+    // synchronises on
+    hipEvent_t fine(hipStream_t st = nullptr) {
+        return ctx->opt_stage_timings ? mark(st) : nullptr;
+    }
     void span(int which, hipEvent_t a, hipEvent_t b) { spans.push_back({which, {a, b}}); }
     float total(int which) {
         float s = 0;
@@ -199,6 +193,85 @@ void set_geometry(nas_ctx *ctx, int n, int dtype) {
     ctx->Mp = (int32_t)nas::round_up(std::max<int64_t>(ctx->Nloc, 1), nas::COST_BM);
 }
 
+// ---- exact int32 traffic on the int8 path (nas::Ovf, nas_internal.h)
+
+// overflow lists of every pod row: ptr[B * Pp + 1] absolute offsets, entries
+// (node, excess); none -> ovf_n = 0 and the plane is the traffic
+int upload_ovf(nas_ctx *ctx, const std::vector<int32_t> &ptr, const std::vector<int32_t> &m,
+               const std::vector<int32_t> &e) {
+    ctx->ovf_n = (int64_t)m.size();
+    if (m.empty()) return NAS_OK;
+    OK(nas::ensure(ctx, ctx->ovf_ptr, ptr.size() * 4));
+    OK(nas::ensure(ctx, ctx->ovf_m, m.size() * 4));
+    OK(nas::ensure(ctx, ctx->ovf_e, e.size() * 4));
+    HIPCK(hipMemcpyAsync(ctx->ovf_ptr.p, ptr.data(), ptr.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->ovf_m.p, m.data(), m.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipMemcpyAsync(ctx->ovf_e.p, e.data(), e.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));  // host vectors die with the caller
+    return NAS_OK;
+}
+
+// after the plane and the lists are on the device: the largest sum_m |WA[p,m]|
+// over pods, for the int32 range check of check_extended
+int finish_traffic_i8(nas_ctx *ctx) {
+    OK(nas::ensure(ctx, ctx->scratch, 64));
+    auto *mx = ctx->scratch.as<unsigned long long>();
+    HIPCK(hipMemsetAsync(mx, 0, 8, ctx->stream));
+    const bool o = ctx->ovf_n > 0;
+    HIPCK(nas::launch_row_abs_max(ctx->stream, ctx->WA.as<signed char>(), (int64_t)ctx->B * ctx->Pp,
+                                  ctx->Kp, o ? ctx->ovf_ptr.as<int32_t>() : nullptr,
+                                  o ? ctx->ovf_m.as<int32_t>() : nullptr,
+                                  o ? ctx->ovf_e.as<int32_t>() : nullptr, mx));
+    unsigned long long h = 0;
+    HIPCK(hipMemcpyAsync(&h, mx, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->wa_abs_row_max = (int64_t)h;
+    return NAS_OK;
+}
+
+// the epilogue's view of the lists (no entries -> ptr null, the kernel skips it)
+nas::Ovf make_ovf(const nas_ctx *ctx, const int32_t *row_pod = nullptr,
+                  const int32_t *row_count = nullptr) {
+    nas::Ovf o;
+    if (ctx->dtype != NAS_DT_I8 || ctx->ovf_n == 0) return o;
+    o.ptr = ctx->ovf_ptr.as<int32_t>();
+    o.m = ctx->ovf_m.as<int32_t>();
+    o.e = ctx->ovf_e.as<int32_t>();
+    o.Lr = ctx->Lr.as<signed char>();
+    o.row_pod = row_pod;
+    o.row_count = row_count;
+    o.N = ctx->N;
+    return o;
+}
+
+// Lr (row-major latency columns for the epilogue's correction), built from Lt
+// on the main stream when lists exist and the latency changed
+int prepare_ovf(nas_ctx *ctx) {
+    if (ctx->dtype != NAS_DT_I8 || ctx->ovf_n == 0 || ctx->lr_valid) return NAS_OK;
+    const size_t per = (size_t)ctx->N * ctx->Mp;
+    OK(nas::ensure(ctx, ctx->Lr, per * ctx->B));
+    for (int b = 0; b < ctx->B; ++b)
+        HIPCK(nas::launch_make_lr(ctx->stream, ctx->Lt.as<signed char>() + (size_t)b * ctx->Mp * ctx->Kp,
+                                  ctx->N, ctx->Mp, ctx->Kp, ctx->Lr.as<signed char>() + b * per));
+    ctx->lr_valid = true;
+    return NAS_OK;
+}
+
+// exact traffic row (n values, each within int32) -> the int8 plane row and
+// the row's overflow entries (node, excess)
+void split_row(const int64_t *v, int n, signed char *plane, std::vector<int32_t> &m,
+               std::vector<int32_t> &e) {
+    for (int j = 0; j < n; ++j) {
+        const int64_t x = v[j];
+        const int64_t c = x < -128 ? -128 : x > 127 ? 127 : x;
+        plane[j] = (signed char)c;
+        if (x != c) {
+            m.push_back(j);
+            e.push_back((int32_t)(x - c));
+        }
+    }
+}
+
 int check_extended(nas_ctx *ctx) {
     if (!ctx->have_L || !ctx->have_cap || !ctx->have_pods || !ctx->have_wa)
         return nas::fail(ctx, NAS_ERR_STATE,
@@ -211,6 +284,12 @@ int check_extended(nas_ctx *ctx) {
         return nas::fail(ctx, NAS_ERR_ARG, "dtypes of latency / traffic differ");
     if (ctx->N != ctx->L_n || ctx->P != ctx->req_P || ctx->dtype != ctx->L_dtype)
         return nas::fail(ctx, NAS_ERR_STATE, "re-upload latency and traffic after resizing");
+    // int8 path: exact int32 costs need sum_m |WA[p,m]| * |L[m,n]| <= INT32_MAX
+    if (ctx->dtype == NAS_DT_I8 && ctx->wa_abs_row_max * (int64_t)ctx->L_abs_max > 0x7fffffffLL)
+        return nas::fail(ctx, NAS_ERR_UNSUPPORTED,
+                         "int8 path: a pod's sum_m |WA[p,m]| * max|L| = " +
+                             std::to_string(ctx->wa_abs_row_max) + " * " +
+                             std::to_string(ctx->L_abs_max) + " exceeds int32");
     return NAS_OK;
 }
 
@@ -305,9 +384,10 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     HIPCK(nas::launch_fit(st, cap, ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp, v.req, p_hi, v.Pp, p_lo,
                           p_hi - p_lo, mask));
     hipEvent_t e1 = tm.fine(st);
+    const nas::Ovf ov = make_ovf(ctx);
     HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, v.WA, ctx->Mp, ctx->Kp, v.Pp, pr0, np,
                                 mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                ctx->Nloc0));
+                                ctx->Nloc0, nullptr, 1, &ov));
     hipEvent_t e2 = tm.fine(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
@@ -351,9 +431,10 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t
     HIPCK(nas::launch_fit(st, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
                           ctx->g_req.as<int32_t>(), R, R, 0, R, mask, &dyn));
     hipEvent_t e2 = tm.mark(st);
+    const nas::Ovf ov = make_ovf(ctx, idx, ctl + 1);  // view row r is pod idx[r]
     HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->g_WA.p, ctx->Mp, ctx->Kp, R, 0, 0,
                                 mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                ctx->Nloc0, &dyn));
+                                ctx->Nloc0, &dyn, 1, &ov));
     hipEvent_t e3 = tm.mark(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     // the last merge writes the fresh lists straight into the pods' own list
@@ -408,9 +489,10 @@ int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi, int32_t *pub = nullptr) {
     auto *mask = ctx->mask.as<uint64_t>();
     HIPCK(nas::launch_fit(sc, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
                           ctx->req.as<int32_t>(), ctx->P, ctx->Pp, 0, RESCORE_PODS, mask, &dyn, B));
+    const nas::Ovf ov = make_ovf(ctx);
     HIPCK(nas::launch_cost_topk(sc, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, ctx->Pp, 0,
                                 0, mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                ctx->Nloc0, &dyn, B));
+                                ctx->Nloc0, &dyn, B, &ov));
     const int n_lists = ctx->Mp / nas::COST_BM;
     if (!exchanging(ctx)) {
         HIPCK(nas::launch_merge(sc, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
@@ -447,9 +529,10 @@ int score_batch(nas_ctx *ctx, Timer &tm) {
     HIPCK(nas::launch_fit(st, ctx->cap.as<int32_t>(), N, 0, N, ctx->Mp, ctx->req.as<int32_t>(), P,
                           Pp, 0, P, mask, nullptr, B));
     hipEvent_t e1 = tm.mark(st);
+    const nas::Ovf ov = make_ovf(ctx);
     HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, Pp, 0, Pp,
                                 mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), 0,
-                                nullptr, B));
+                                nullptr, B, &ov));
     hipEvent_t e2 = tm.mark(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
@@ -483,7 +566,6 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
     HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), Pp, 0, P, ctx->cap.as<int32_t>(), N,
                              ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt, B));
-    for (int r = 0; r < RESCORE_SLOTS_LAST; ++r) OK(rescore_slot(ctx, st, P));
     tm.span(T_COMMIT, e3, tm.mark(st));
     int slots = 0;
     while (true) {
@@ -542,55 +624,69 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
     return NAS_OK;
 }
 
-// device-side rescore slots behind a chunk's commit (NAS_RESCORE_SLOTS
-// overrides the count for every chunk; read once)
-int rescore_slots(bool last) {
-    static const int n = [] {
-        const char *e = std::getenv("NAS_RESCORE_SLOTS");
-        return e ? std::max(0, std::atoi(e)) : -1;
-    }();
-    if (n >= 0) return n;
-    return last ? RESCORE_SLOTS_LAST : RESCORE_SLOTS;
+// Abort every communicator of a context whose collective missed its deadline:
+// the stuck collective kernels return, later calls fail fast (bind).
+void abort_comms(nas_ctx *ctx) {
+    for (ncclComm **c : {&ctx->comm, &ctx->comm2, &ctx->comm_c}) {
+        if (*c) (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(*c));
+        *c = nullptr;
+    }
+    ctx->poisoned = true;
 }
 
-// Wait for an event: hipEventSynchronize, or (NAS_WAIT=spin) by polling it
-// on this host core -- measured equal on the G = 8 rehearsal (1.38-1.41 ms
-// per pass either way), so the blocking wait is the default.
+// Wait for an event.  Without a communicator: hipEventSynchronize.  With one
+// (the call issued collectives that other ranks must join), poll under the
+// NAS_OPT_COMM_TIMEOUT_MS deadline -- a rank whose peers never arrive would
+// otherwise block in the collective forever -- and on expiry abort the
+// communicators and poison the context.  (Polling measured equal to the
+// blocking wait on the G = 8 rehearsal: 1.38-1.41 ms per pass either way.)
 int wait_event(nas_ctx *ctx, hipEvent_t e) {
-    static const bool block = [] {
-        const char *v = std::getenv("NAS_WAIT");
-        return !(v && std::strcmp(v, "spin") == 0);
-    }();
-    if (block) {
+    if (!ctx->comm || ctx->opt_comm_timeout_ms <= 0) {
         HIPCK(hipEventSynchronize(e));
         return NAS_OK;
     }
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    const auto limit = std::chrono::milliseconds(ctx->opt_comm_timeout_ms);
     for (;;) {
         const hipError_t r = hipEventQuery(e);
         if (r == hipSuccess) return NAS_OK;
         if (r != hipErrorNotReady) return nas::hip_fail(ctx, r, "hipEventQuery");
-        __builtin_ia32_pause();
+        const auto waited = clk::now() - t0;
+        if (waited > limit) {
+            abort_comms(ctx);
+            return nas::fail(ctx, NAS_ERR_COMM,
+                             "collective did not complete within " +
+                                 std::to_string(ctx->opt_comm_timeout_ms) +
+                                 " ms (NAS_OPT_COMM_TIMEOUT_MS): communicators aborted, "
+                                 "context poisoned");
+        }
+        if (waited < std::chrono::milliseconds(2)) __builtin_ia32_pause();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
 }
 
-// copy each chunk's results to the host right behind its commit (default)
-// or all of them at the end (NAS_CHUNK_COPIES=0)
-bool chunk_copies() {
-    static const bool v = [] {
-        const char *e = std::getenv("NAS_CHUNK_COPIES");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    return v;
+// stream synchronisation of the calls that may have issued collectives
+int sync_stream(nas_ctx *ctx, hipStream_t st) {
+    if (!ctx->comm) {
+        HIPCK(hipStreamSynchronize(st));
+        return NAS_OK;
+    }
+    hipEvent_t e = nullptr;
+    HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    hipError_t r = hipEventRecord(e, st);
+    int rc = r == hipSuccess ? wait_event(ctx, e) : nas::hip_fail(ctx, r, "hipEventRecord");
+    (void)hipEventDestroy(e);
+    return rc;
 }
 
-// where a chunk's merge / exchange runs in nas_place: on the commit stream
-// (default) or behind its cost launch on the scoring stream (NAS_MERGE_ON=score)
-bool merge_on_commit_stream() {
-    static const bool v = [] {
-        const char *e = std::getenv("NAS_MERGE_ON");
-        return !(e && std::strcmp(e, "score") == 0);
-    }();
-    return v;
+// NAS_OPT_INJECT_STALL_MS (tests): delay the stream a call waits on, once,
+// behind the call's collectives (so the abort it provokes finds them done)
+void inject_stall(nas_ctx *ctx, hipStream_t st) {
+    if (ctx->opt_inject_stall_ms > 0) {
+        (void)nas::launch_stall(st, ctx->opt_inject_stall_ms);
+        ctx->opt_inject_stall_ms = 0;
+    }
 }
 
 // pods per pipelined scoring chunk starting at pod lo: at least 32 pod
@@ -599,15 +695,9 @@ bool merge_on_commit_stream() {
 // is 32 tiles, so the commit stream starts early, and the last is at most
 // about 32, so the commit left after the scoring ends (the serial tail, which
 // matters most on a node shard's short scoring) is short.
+constexpr int CHUNK_WORKGROUPS = 512;  // cost workgroups per big chunk (measured best)
 int chunk_pods(const nas_ctx *ctx, int c, int lo) {
-    static const int wgs = [] {
-        const char *e = std::getenv("NAS_CHUNK_WG");  // tuning knob: workgroups per big chunk
-        return e && std::atoi(e) > 0 ? std::atoi(e) : 512;
-    }();
-    static const int env_mode = [] {
-        const char *e = std::getenv("NAS_CHUNK_MODE");  // tuning knob, see below
-        return e ? std::atoi(e) : -1;
-    }();
+    const int wgs = CHUNK_WORKGROUPS;
     const int n_mt = ctx->Mp / nas::COST_BM;
     const int big = std::max(32, (wgs + n_mt - 1) / n_mt);
     // 32-tile chunks (whole waves of workgroups at 8+ node tiles) with a
@@ -615,17 +705,13 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     // with few node tiles), equal chunks: on rank 0 of a G = 8 rehearsal
     // 1.45 ms vs 1.56 ms per C3 pass, while at G = 1 the 32-tile form is
     // 2.5% ahead (8.15 vs 8.37 ms)
-    const int mode = env_mode >= 0 ? env_mode : (big > 32 ? 2 : 0);
+    const int mode = big > 32 ? 2 : 0;
     const int left = (ctx->P - lo + nas::COST_BN - 1) / nas::COST_BN;  // pod tiles left
     int tiles = c == 0 ? 32 : big;
     // a pass whose pods fit one big chunk (C2: 40 pod tiles on 4 node tiles)
     // is one chunk: pipelining its short tail would save less than the
-    // cross-stream hops and launches it adds (NAS_CHUNK_WHOLE=0 turns this off)
-    static const bool whole = [] {
-        const char *e = std::getenv("NAS_CHUNK_WHOLE");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    if (whole && c == 0 && left <= big) tiles = left;
+    // cross-stream hops and launches it adds (device time 0.96 -> 0.92 ms, C2)
+    if (c == 0 && left <= big) tiles = left;
     if (mode == 0) {
         // a big last chunk is split in two so that the last is 32 tiles (unless
         // the first part would be a sliver of under 16)
@@ -724,7 +810,7 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
 void nas_destroy(nas_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream_commit}) (void)hipStreamSynchronize(st);
     DevBuf *bufs[] = {&ctx->snap[0], &ctx->snap[1], &ctx->snap[2], &ctx->snap[3], &ctx->snap[4],
                       &ctx->snap[5], &ctx->order1, &ctx->pos1, &ctx->order2, &ctx->pos2,
                       &ctx->pod_snap, &ctx->best, &ctx->winners, &ctx->snap_best, &ctx->snap_win,
@@ -735,7 +821,8 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
                       &ctx->g_words, &ctx->g_idx, &ctx->g_WA, &ctx->g_req, &ctx->g_key,
                       &ctx->g_bound, &ctx->g_gk, &ctx->g_gb, &ctx->status, &ctx->scratch,
-                      &ctx->vote_part, &ctx->vote_gather, &ctx->xsend[0], &ctx->xsend[1]};
+                      &ctx->vote_part, &ctx->vote_gather, &ctx->xsend[0], &ctx->xsend[1],
+                      &ctx->ovf_ptr, &ctx->ovf_m, &ctx->ovf_e, &ctx->Lr};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
@@ -754,6 +841,33 @@ int nas_get_timings(nas_ctx *ctx, nas_timings *out) {
     if (!ctx || !out) return NAS_ERR_ARG;
     *out = ctx->timings;
     return NAS_OK;
+}
+
+int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value) {
+    if (!ctx) return NAS_ERR_ARG;
+    ctx->err.clear();
+    switch (key) {
+    case NAS_OPT_STAGE_TIMINGS:
+        if (value != 0 && value != 1) break;
+        ctx->opt_stage_timings = value != 0;
+        return NAS_OK;
+    case NAS_OPT_COMM_TIMEOUT_MS:
+        if (value < 0) break;
+        ctx->opt_comm_timeout_ms = value;
+        return NAS_OK;
+    case NAS_OPT_REHEARSE_WORLD:
+        if (value < 0 || value > 64) break;
+        if (ctx->comm) return nas::fail(ctx, NAS_ERR_STATE, "set NAS_OPT_REHEARSE_WORLD before nas_comm_init");
+        ctx->opt_rehearse_world = (int32_t)value;
+        return NAS_OK;
+    case NAS_OPT_INJECT_STALL_MS:
+        if (value < 0 || value > 60000) break;
+        ctx->opt_inject_stall_ms = value;
+        return NAS_OK;
+    default:
+        return nas::fail(ctx, NAS_ERR_ARG, "nas_set_option: unknown key " + std::to_string(key));
+    }
+    return nas::fail(ctx, NAS_ERR_ARG, "nas_set_option: value out of range for key " + std::to_string(key));
 }
 
 // ---------------------------------------------------------------- reference
@@ -954,8 +1068,10 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
     HIPCK(hipMemcpyAsync(stage, best_d, (size_t)P * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (winners_out)
         HIPCK(hipMemcpyAsync(stage + P, win_d, (size_t)P * 24, hipMemcpyDeviceToHost, ctx->stream));
+    if (ctx->snap_sharded && ctx->comm) inject_stall(ctx, ctx->stream);
     hipEvent_t c = tm.mark();
-    HIPCK(hipStreamSynchronize(ctx->stream));
+    if (ctx->snap_sharded) OK(sync_stream(ctx, ctx->stream));
+    else HIPCK(hipStreamSynchronize(ctx->stream));
     std::memcpy(best_out, stage, (size_t)P * 4);
     if (winners_out) std::memcpy(winners_out, stage + P, (size_t)P * 24);
     tm.span(T_VOTE, a, b);
@@ -970,9 +1086,13 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
     OK(bind(ctx));
     if (!L || n <= 0 || (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
         return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_latency: L / n / dtype");
-    if ((int64_t)n * 127 * 128 >= (int64_t)1 << 31 && dtype == NAS_DT_I8)
-        return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "int8 path: n too large for exact int32 costs");
     set_geometry(ctx, n, dtype);
+    if (dtype == NAS_DT_I8) {  // max |L| over the whole matrix (the same on every rank)
+        const auto *l = static_cast<const signed char *>(L);
+        int mx = 0;
+        for (size_t i = 0, e = (size_t)ctx->B * n * n; i < e; ++i) mx = std::max(mx, std::abs((int)l[i]));
+        ctx->L_abs_max = mx;
+    }
     if (ctx->have_wa && (ctx->wa_n != n || ctx->wa_dtype != dtype)) ctx->have_wa = false;
     const size_t e = esz(dtype);
     const size_t lt_b = (size_t)ctx->Mp * ctx->Kp * e;  // one cluster's Lt
@@ -994,6 +1114,8 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
     ctx->L_n = n;
     ctx->L_dtype = dtype;
     ctx->synth_valid = false;
+    ctx->lr_valid = false;
+    ctx->scored = false;
     return NAS_OK;
 }
 
@@ -1066,11 +1188,13 @@ int nas_upload_pods(nas_ctx *ctx, const int32_t *rc, const int32_t *rm, const in
         ctx->P = P;
         ctx->Pp = Pp;
     }
+    if (P != ctx->req_P) ctx->scored = false;  // lists of another pod set
     ctx->req_P = P;
     ctx->have_pods = true;
     return NAS_OK;
 }
 
+// dtype here is the COMPUTE dtype (NAS_DT_I8 for int8 / int32 traffic)
 static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
     if (P <= 0 || n <= 0 || (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
         return nas::fail(ctx, NAS_ERR_ARG, "traffic: P / n / dtype");
@@ -1086,12 +1210,49 @@ static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
     ctx->wa_P = P;
     ctx->wa_n = n;
     ctx->wa_dtype = dtype;
+    ctx->ovf_n = 0;
+    ctx->wa_abs_row_max = 0;
+    ctx->scored = false;  // the lists (and their buffers' sizes) belong to the old inputs
+    ctx->have_wa = false;
     return NAS_OK;
 }
 
 int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_t P, int32_t n) {
     OK(bind(ctx));
     if (!WA) return nas::fail(ctx, NAS_ERR_ARG, "WA null");
+    if (dtype == NAS_DT_I32) {
+        // exact int32 traffic: the int8 plane (clamped) + overflow lists,
+        // split on the host in row blocks
+        OK(traffic_common(ctx, NAS_DT_I8, P, n));
+        const auto *src = static_cast<const int32_t *>(WA);
+        const int B = ctx->B, Pp = ctx->Pp, Kp = ctx->Kp;
+        std::vector<int32_t> ptr((size_t)B * Pp + 1, 0), om, oe;
+        const int rows_blk = std::max(1, (int)std::min<int64_t>(P, (64 << 20) / std::max(1, n)));
+        std::vector<signed char> plane((size_t)rows_blk * n);
+        std::vector<int64_t> row(n);
+        for (int b = 0; b < B; ++b)
+            for (int p0 = 0; p0 < P; p0 += rows_blk) {
+                const int nr = std::min(rows_blk, P - p0);
+                for (int i = 0; i < nr; ++i) {
+                    const int32_t *r = src + ((size_t)b * P + p0 + i) * n;
+                    for (int j = 0; j < n; ++j) row[j] = r[j];
+                    split_row(row.data(), n, plane.data() + (size_t)i * n, om, oe);
+                    ptr[(size_t)b * Pp + p0 + i + 1] = (int32_t)om.size();
+                }
+                HIPCK(hipMemcpy2DAsync(ctx->WA.as<char>() + ((size_t)b * Pp + p0) * Kp, (size_t)Kp,
+                                       plane.data(), (size_t)n, (size_t)n, nr,
+                                       hipMemcpyHostToDevice, ctx->stream));
+                HIPCK(hipStreamSynchronize(ctx->stream));  // plane is reused
+            }
+        // padding rows carry the running offset
+        for (size_t r = 1; r < ptr.size(); ++r) ptr[r] = std::max(ptr[r], ptr[r - 1]);
+        if (om.size() > 0x7fffffffu) return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "too many overflow entries");
+        OK(upload_ovf(ctx, ptr, om, oe));
+        OK(finish_traffic_i8(ctx));
+        ctx->have_wa = true;
+        ctx->synth_valid = false;
+        return NAS_OK;
+    }
     OK(traffic_common(ctx, dtype, P, n));
     const size_t e = esz(dtype);
     for (size_t b = 0; b < (size_t)ctx->B; ++b)
@@ -1099,6 +1260,7 @@ int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_
                                static_cast<const char *>(WA) + b * P * n * e, (size_t)n * e,
                                (size_t)n * e, P, hipMemcpyHostToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
+    if (dtype == NAS_DT_I8) OK(finish_traffic_i8(ctx));
     ctx->have_wa = true;
     ctx->synth_valid = false;
     return NAS_OK;
@@ -1109,26 +1271,95 @@ int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *
     OK(bind(ctx));
     if (!row_ptr || nnz < 0 || (nnz > 0 && (!peer_node || !weight)))
         return nas::fail(ctx, NAS_ERR_ARG, "csr arrays");
+    if (dtype != NAS_DT_I8 && dtype != NAS_DT_I32 && dtype != NAS_DT_BF16)
+        return nas::fail(ctx, NAS_ERR_ARG, "csr weight dtype");
     if (ctx->B > 1) return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "CSR traffic with a cluster batch");
-    if (row_ptr[0] != 0 || row_ptr[P] != nnz) return nas::fail(ctx, NAS_ERR_ARG, "row_ptr bounds");
+    if (P <= 0 || row_ptr[0] != 0 || row_ptr[P] != nnz)
+        return nas::fail(ctx, NAS_ERR_ARG, "row_ptr bounds");
     for (int p = 0; p < P; ++p)
         if (row_ptr[p + 1] < row_ptr[p]) return nas::fail(ctx, NAS_ERR_ARG, "row_ptr not monotone");
+    if (dtype != NAS_DT_BF16) {
+        // exact integer aggregation on the host (int64 sums, then int32 range):
+        // the plane entries are scattered on the device, the rest is overflow
+        OK(traffic_common(ctx, NAS_DT_I8, P, n));
+        std::vector<int32_t> ptr((size_t)ctx->Pp + 1, 0), om, oe, tp, tn;
+        std::vector<signed char> tv;
+        std::vector<std::pair<int32_t, int64_t>> agg;
+        for (int p = 0; p < P; ++p) {
+            agg.clear();
+            for (int64_t x = row_ptr[p]; x < row_ptr[p + 1]; ++x) {
+                const int32_t m = peer_node[x];
+                if (m < 0 || m >= n) continue;  // unbound peer (or off-cluster): skipped
+                const int64_t w = dtype == NAS_DT_I8 ? (int64_t) static_cast<const int8_t *>(weight)[x]
+                                                     : (int64_t) static_cast<const int32_t *>(weight)[x];
+                agg.push_back({m, w});
+            }
+            std::sort(agg.begin(), agg.end(),
+                      [](const auto &a, const auto &b) { return a.first < b.first; });
+            for (size_t i = 0; i < agg.size();) {
+                const int32_t m = agg[i].first;
+                int64_t v = 0;
+                for (; i < agg.size() && agg[i].first == m; ++i) v += agg[i].second;
+                if (v < INT32_MIN || v > INT32_MAX)
+                    return nas::fail(ctx, NAS_ERR_UNSUPPORTED,
+                                     "traffic of pod " + std::to_string(p) + " to node " +
+                                         std::to_string(m) + " exceeds int32");
+                if (v == 0) continue;
+                const int64_t c = v < -128 ? -128 : v > 127 ? 127 : v;
+                tp.push_back(p);
+                tn.push_back(m);
+                tv.push_back((signed char)c);
+                if (v != c) {
+                    om.push_back(m);
+                    oe.push_back((int32_t)(v - c));
+                }
+            }
+            ptr[p + 1] = (int32_t)om.size();
+        }
+        for (size_t r = (size_t)P + 1; r < ptr.size(); ++r) ptr[r] = ptr[r - 1];
+        DevBuf dp, dn, dv;
+        int rc = nas::ensure(ctx, dp, tp.size() * 4 + 4);
+        if (rc == NAS_OK) rc = nas::ensure(ctx, dn, tn.size() * 4 + 4);
+        if (rc == NAS_OK) rc = nas::ensure(ctx, dv, tv.size() + 4);
+        hipError_t he = hipSuccess;
+        if (rc == NAS_OK && !tp.empty()) {
+            he = hipMemcpyAsync(dp.p, tp.data(), tp.size() * 4, hipMemcpyHostToDevice, ctx->stream);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(dn.p, tn.data(), tn.size() * 4, hipMemcpyHostToDevice, ctx->stream);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(dv.p, tv.data(), tv.size(), hipMemcpyHostToDevice, ctx->stream);
+            if (he == hipSuccess)
+                he = nas::launch_plane_scatter(ctx->stream, dp.as<int32_t>(), dn.as<int32_t>(),
+                                               dv.as<signed char>(), (int64_t)tp.size(), ctx->Kp,
+                                               ctx->WA.as<signed char>());
+        }
+        (void)hipStreamSynchronize(ctx->stream);
+        for (DevBuf *b : {&dp, &dn, &dv})
+            if (b->p) (void)hipFree(b->p);
+        if (rc != NAS_OK) return rc;
+        if (he != hipSuccess) return nas::hip_fail(ctx, he, "csr plane scatter");
+        OK(upload_ovf(ctx, ptr, om, oe));
+        OK(finish_traffic_i8(ctx));
+        ctx->have_wa = true;
+        ctx->synth_valid = false;
+        return NAS_OK;
+    }
     OK(traffic_common(ctx, dtype, P, n));
     DevBuf rp, pn, w;
     int rc = nas::ensure(ctx, rp, (size_t)(P + 1) * 4);
     if (rc == NAS_OK) rc = nas::ensure(ctx, pn, (size_t)nnz * 4);
-    if (rc == NAS_OK) rc = nas::ensure(ctx, w, (size_t)nnz * esz(dtype));
+    if (rc == NAS_OK) rc = nas::ensure(ctx, w, (size_t)nnz * 2);
     hipError_t he = hipSuccess;
     if (rc == NAS_OK) {
         he = hipMemcpyAsync(rp.p, row_ptr, (size_t)(P + 1) * 4, hipMemcpyHostToDevice, ctx->stream);
         if (he == hipSuccess && nnz)
             he = hipMemcpyAsync(pn.p, peer_node, (size_t)nnz * 4, hipMemcpyHostToDevice, ctx->stream);
         if (he == hipSuccess && nnz)
-            he = hipMemcpyAsync(w.p, weight, (size_t)nnz * esz(dtype), hipMemcpyHostToDevice,
-                                ctx->stream);
+            he = hipMemcpyAsync(w.p, weight, (size_t)nnz * 2, hipMemcpyHostToDevice, ctx->stream);
         if (he == hipSuccess)
-            he = nas::launch_csr_aggregate(ctx->stream, rp.as<int32_t>(), pn.as<int32_t>(), w.p,
-                                           dtype, P, n, ctx->Kp, ctx->WA.p);
+            he = nas::launch_csr_aggregate_bf16(ctx->stream, rp.as<int32_t>(), pn.as<int32_t>(),
+                                                w.as<uint16_t>(), P, n, ctx->Kp,
+                                                ctx->WA.as<uint16_t>());
         if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
     }
     (void)hipStreamSynchronize(ctx->stream);
@@ -1170,11 +1401,13 @@ int nas_score(nas_ctx *ctx) {
     OK(bind(ctx));
     OK(check_extended(ctx));
     OK(alloc_extended(ctx));
+    OK(prepare_ovf(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     if (ctx->B > 1) OK(score_batch(ctx, tm));
     else OK(score_range(ctx, tm, 0, ctx->P));
-    HIPCK(hipStreamSynchronize(ctx->stream));
+    if (ctx->comm) inject_stall(ctx, ctx->stream);
+    OK(sync_stream(ctx, ctx->stream));
     ctx->timings.fit_ms = tm.total(T_FIT);
     ctx->timings.cost_ms = tm.total(T_COST);
     ctx->timings.merge_ms = tm.total(T_MERGE);
@@ -1190,11 +1423,10 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
                          "nas_place on a shard needs nas_comm_init (nas_set_shard scores only)");
     if (!node_out) return nas::fail(ctx, NAS_ERR_ARG, "node_out null");
     OK(alloc_extended(ctx));
+    OK(prepare_ovf(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     if (ctx->B > 1) return place_batch(ctx, tm, node_out, cost_out, int_score_out);
-    static const bool trace_host = std::getenv("NAS_TRACE_HOST") != nullptr;  // diagnostic
-    const auto h0 = std::chrono::steady_clock::now();
     hipStream_t st = ctx->stream, sc = ctx->stream_commit;
     const int P = ctx->P, N = ctx->N;
     int32_t *halt = ctx->status.as<int32_t>();
@@ -1236,52 +1468,41 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // a one-chunk pass without a communicator has nothing to pipeline: its
     // merge / commit / copies stay on the scoring stream, which saves the
     // cross-stream event hops (~15-20 us each) that dominate a small pass
-    static const bool one_stream = [] {  // NAS_ONE_STREAM=0 turns this off, for A/B runs
-        const char *e = std::getenv("NAS_ONE_STREAM");
-        return !(e && std::strcmp(e, "0") == 0);
-    }();
-    if (one_stream && chunks.size() == 1 && !ctx->comm) sc = st;
-    const bool split = merge_on_commit_stream();
+    // (C1 extended 0.41 -> 0.385 ms per nas_place)
+    if (chunks.size() == 1 && !ctx->comm) sc = st;
     std::vector<hipEvent_t> scored(chunks.size());
-    auto score_chunk = [&](size_t c) -> int {
-        // two scoring streams (each with its own communicator when sharded):
-        // a chunk's tail blocks overlap the next chunk (a third scoring
-        // stream measured 5% slower at G = 1 and 6-25% at G = 8)
+    // fit + cost only on the two scoring streams (a chunk's tail blocks overlap
+    // the next chunk; a third scoring stream measured 5% slower at G = 1 and
+    // 6-25% at G = 8); the commit stream merges (and exchanges, over its own
+    // communicator) each chunk right before committing it, so no cost launch
+    // ever waits behind a merge or an all-gather
+    for (size_t c = 0; c < chunks.size(); ++c) {
         hipStream_t ss = (c & 1) ? ctx->stream2 : st;
-        OK(score_range(ctx, tm, chunks[c].first, chunks[c].second, ss, score_cap, nullptr, !split));
+        OK(score_range(ctx, tm, chunks[c].first, chunks[c].second, ss, score_cap, nullptr, false));
         scored[c] = tm.mark(ss);
-        return NAS_OK;
-    };
-    if (split)  // fit + cost only: the commit stream merges (and exchanges, over
-                // its own communicator) each chunk right before committing it
-        for (size_t c = 0; c < chunks.size(); ++c) OK(score_chunk(c));
+    }
     for (size_t c = 0; c < chunks.size(); ++c) {
         const int lo = chunks[c].first, hi = chunks[c].second;
-        if (!split) OK(score_chunk(c));
         HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
-        if (split) OK(merge_range(ctx, tm, lo, hi, sc, ctx->comm_c, 0, main_view(ctx)));
+        OK(merge_range(ctx, tm, lo, hi, sc, ctx->comm_c, 0, main_view(ctx)));
         hipEvent_t c0 = tm.fine(sc);
         HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
                                  1, pub));
         tm.span(T_COMMIT, c0, tm.fine(sc));
-        for (int r = 0, n = rescore_slots(hi == P); r < n; ++r)
-            OK(gathered_slot(ctx, tm, sc, ctx->comm_c, pub, hi));
         // this chunk's results go to the pinned stage right behind its
         // commit, and the host unpacks them while later chunks still run
-        if (chunk_copies()) {
-            HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo,
+        HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo, (size_t)(hi - lo) * 4,
+                             hipMemcpyDeviceToHost, sc));
+        if (want_raw)
+            HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
                                  (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, sc));
-            if (want_raw)
-                HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
-                                     (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, sc));
-            landed.push_back({lo, hi, tm.mark(sc)});
-        }
+        landed.push_back({lo, hi, tm.mark(sc)});
     }
     HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
     HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
-    const auto h1 = std::chrono::steady_clock::now();
+    if (ctx->comm) inject_stall(ctx, st);  // behind every collective of the pass
     hipEvent_t t1 = nullptr;
     auto fetch = [&]() -> int {
         // halt[0..2]: halt word, slot resumes, commit rounds; ctl[2]: pods rescored
@@ -1292,8 +1513,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
             HIPCK(hipMemcpyAsync(stage + P, ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost,
                                  st));
         t1 = tm.mark(st);
-        HIPCK(hipStreamSynchronize(st));
-        return NAS_OK;
+        return wait_event(ctx, t1);
     };
     int unsched = 0;
     auto unpack = [&](int lo, int hi) {
@@ -1313,26 +1533,12 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // everything is fetched and unpacked again.
     HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
-    if (landed.empty()) {  // NAS_CHUNK_COPIES=0: one copy of everything at the end
-        HIPCK(hipMemcpyAsync(stage, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
-        if (want_raw)
-            HIPCK(hipMemcpyAsync(stage + P, ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost,
-                                 st));
-        landed.push_back({0, P, nullptr});
-    }
     t1 = tm.mark(st);
-    if (!landed.back().ev) landed.back().ev = t1;
     for (const Landed &l : landed) {
         OK(wait_event(ctx, l.ev));
         unpack(l.lo, l.hi);
     }
     OK(wait_event(ctx, t1));  // t1 follows everything on st (the status copies)
-    if (trace_host) {
-        const auto h2 = std::chrono::steady_clock::now();
-        auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-        std::fprintf(stderr, "nas_place host: enqueue %.1f us, wait+unpack %.1f us, chunks %zu\n",
-                     us(h0, h1), us(h1, h2), chunks.size());
-    }
     int checks = 0;
     while (hs[0] >= 0) {
         // still halted after the pipeline: more gathered slots, checked in batches
@@ -1399,10 +1605,12 @@ int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi) {
     if (p_lo < 0 || p_hi > ctx->P || p_lo >= p_hi)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_score_range: pod range");
     OK(alloc_extended(ctx));
+    OK(prepare_ovf(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     OK(score_range(ctx, tm, p_lo, p_hi));
-    HIPCK(hipStreamSynchronize(ctx->stream));
+    if (ctx->comm) inject_stall(ctx, ctx->stream);
+    OK(sync_stream(ctx, ctx->stream));
     ctx->timings.fit_ms = tm.total(T_FIT);
     ctx->timings.cost_ms = tm.total(T_COST);
     ctx->timings.merge_ms = tm.total(T_MERGE);
@@ -1412,7 +1620,7 @@ int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi) {
 
 static int keys_range_ok(nas_ctx *ctx, int32_t p_lo, int32_t n, const void *keys,
                          const void *bounds) {
-    if (!ctx->cand_key.p) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
+    if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
     if (p_lo < 0 || n < 0 || p_lo + n > ctx->P || (n > 0 && (!keys || !bounds)))
         return nas::fail(ctx, NAS_ERR_ARG, "candidate key range");
     return NAS_OK;
@@ -1436,7 +1644,10 @@ int nas_set_candidate_keys(nas_ctx *ctx, int32_t p_lo, int32_t n, const uint64_t
                            const uint64_t *bounds) {
     OK(bind(ctx));
     OK(no_batch(ctx, "candidate key ranges"));
-    OK(keys_range_ok(ctx, p_lo, n, keys, bounds));
+    OK(check_extended(ctx));
+    OK(alloc_extended(ctx));  // lists sized for the current pods
+    if (p_lo < 0 || n < 0 || p_lo + n > ctx->P || (n > 0 && (!keys || !bounds)))
+        return nas::fail(ctx, NAS_ERR_ARG, "candidate key range");
     // the commit relies on sorted lists with in-range node ids
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         const uint64_t *k = keys + i * KC;
@@ -1465,6 +1676,7 @@ int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out
     if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "nas_commit needs candidate lists");
     if (!node_out || !stop_out || p_begin < 0 || p_begin > ctx->P)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_commit arguments");
+    OK(alloc_extended(ctx));  // (scored implies they match; cheap when they do)
     const int P = ctx->P;
     *stop_out = P;
     if (p_begin == P) return NAS_OK;
@@ -1530,8 +1742,9 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     ctx->world = world;
     ctx->virtual_shard = false;
     ctx->rehearse = 0;
-    if (const char *g = std::getenv("NAS_REHEARSE_WORLD"); g && world == 1 && std::atoi(g) > 1) {
-        ctx->rehearse = std::atoi(g);  // diagnostic: one rank of a G-GPU pass (nas_internal.h)
+    if (ctx->opt_rehearse_world > 1 && world == 1) {
+        // diagnostic (NAS_OPT_REHEARSE_WORLD): one rank of a G-GPU pass
+        ctx->rehearse = ctx->opt_rehearse_world;
         ctx->world = ctx->rehearse;
     }
     ncclUniqueId uid;
@@ -1671,6 +1884,50 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
     HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)B * 3 * n_nodes * 4,
                          hipMemcpyDeviceToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
+    ctx->ovf_n = 0;
+    ctx->lr_valid = false;
+    ctx->scored = false;
+    if (dtype == NAS_DT_I8) {
+        // exact traffic: peer aggregates beyond the int8 plane go to the
+        // overflow lists (counts, host prefix sum, entries)
+        const size_t rows = (size_t)B * ctx->Pp;
+        DevBuf cnt;
+        OK(nas::ensure(ctx, cnt, rows * 4));
+        hipError_t he = hipMemsetAsync(cnt.p, 0, rows * 4, ctx->stream);
+        for (int b = 0; b < B && he == hipSuccess; ++b)
+            he = nas::launch_synth_overflow(ctx->stream, seed + b, n_nodes, P, peers, ctx->Kp, 0,
+                                            nullptr, cnt.as<int32_t>() + (size_t)b * ctx->Pp,
+                                            nullptr, nullptr, nullptr);
+        std::vector<int32_t> c(rows), ptr(rows + 1, 0);
+        if (he == hipSuccess)
+            he = hipMemcpyAsync(c.data(), cnt.p, rows * 4, hipMemcpyDeviceToHost, ctx->stream);
+        if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+        (void)hipFree(cnt.p);
+        if (he != hipSuccess) return nas::hip_fail(ctx, he, "synth overflow counts");
+        int64_t tot = 0;
+        for (size_t r = 0; r < rows; ++r) {
+            tot += c[r];
+            if (tot > 0x7fffffff) return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "too many overflow entries");
+            ptr[r + 1] = (int32_t)tot;
+        }
+        if (tot > 0) {
+            OK(nas::ensure(ctx, ctx->ovf_ptr, ptr.size() * 4));
+            OK(nas::ensure(ctx, ctx->ovf_m, (size_t)tot * 4));
+            OK(nas::ensure(ctx, ctx->ovf_e, (size_t)tot * 4));
+            HIPCK(hipMemcpyAsync(ctx->ovf_ptr.p, ptr.data(), ptr.size() * 4, hipMemcpyHostToDevice,
+                                 ctx->stream));
+            for (int b = 0; b < B; ++b)
+                HIPCK(nas::launch_synth_overflow(ctx->stream, seed + b, n_nodes, P, peers, ctx->Kp, 1,
+                                                 nullptr, nullptr,
+                                                 ctx->ovf_ptr.as<int32_t>() + (size_t)b * ctx->Pp,
+                                                 ctx->ovf_m.as<int32_t>(), ctx->ovf_e.as<int32_t>()));
+            HIPCK(hipStreamSynchronize(ctx->stream));
+            ctx->ovf_n = tot;
+        }
+        ctx->L_abs_max = 127;  // bound of the synthetic latency classes (<= 104), same on every rank
+        ctx->B = B;
+        OK(finish_traffic_i8(ctx));
+    }
     ctx->have_L = ctx->have_cap = ctx->have_pods = ctx->have_wa = true;
     ctx->L_n = ctx->cap_n = ctx->wa_n = n_nodes;
     ctx->req_P = ctx->wa_P = P;
@@ -1701,10 +1958,38 @@ int nas_read_inputs(nas_ctx *ctx, int32_t p0, int32_t np, void *WA_rows, void *L
     const size_t e = esz(ctx->dtype);
     if (WA_rows) {
         if (p0 < 0 || np < 0 || p0 + np > ctx->P) return nas::fail(ctx, NAS_ERR_ARG, "pod rows");
-        if (np)
+        if (np && ctx->dtype != NAS_DT_I8) {
             HIPCK(hipMemcpy2DAsync(WA_rows, (size_t)N * e, ctx->WA.as<char>() + (size_t)p0 * ctx->Kp * e,
                                    (size_t)ctx->Kp * e, (size_t)N * e, np, hipMemcpyDeviceToHost,
                                    ctx->stream));
+        } else if (np) {
+            // int8 scoring: the exact int32 traffic = plane + overflow entries
+            std::vector<signed char> pl((size_t)np * N);
+            HIPCK(hipMemcpy2DAsync(pl.data(), (size_t)N, ctx->WA.as<char>() + (size_t)p0 * ctx->Kp,
+                                   (size_t)ctx->Kp, (size_t)N, np, hipMemcpyDeviceToHost, ctx->stream));
+            std::vector<int32_t> ptr(np + 1, 0), om, oe;
+            if (ctx->ovf_n) {
+                HIPCK(hipMemcpyAsync(ptr.data(), ctx->ovf_ptr.as<int32_t>() + p0, (size_t)(np + 1) * 4,
+                                     hipMemcpyDeviceToHost, ctx->stream));
+                HIPCK(hipStreamSynchronize(ctx->stream));
+                const size_t ne = (size_t)(ptr[np] - ptr[0]);
+                om.resize(ne);
+                oe.resize(ne);
+                if (ne) {
+                    HIPCK(hipMemcpyAsync(om.data(), ctx->ovf_m.as<int32_t>() + ptr[0], ne * 4,
+                                         hipMemcpyDeviceToHost, ctx->stream));
+                    HIPCK(hipMemcpyAsync(oe.data(), ctx->ovf_e.as<int32_t>() + ptr[0], ne * 4,
+                                         hipMemcpyDeviceToHost, ctx->stream));
+                }
+            }
+            HIPCK(hipStreamSynchronize(ctx->stream));
+            auto *out = static_cast<int32_t *>(WA_rows);
+            for (size_t i = 0; i < pl.size(); ++i) out[i] = pl[i];
+            if (ctx->ovf_n)
+                for (int r = 0; r < np; ++r)
+                    for (int j = ptr[r]; j < ptr[r + 1]; ++j)
+                        out[(size_t)r * N + om[j - ptr[0]]] += oe[j - ptr[0]];
+        }
     }
     if (L) {
         if (ctx->synth_valid) {

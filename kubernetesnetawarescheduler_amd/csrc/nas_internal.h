@@ -40,6 +40,24 @@ constexpr int STATUS_INTS = 4;
 // in the low word; ascending key == ascending (cost, node).
 constexpr uint64_t KEY_INVALID = ~0ull;
 
+// Exact int32 traffic on the int8 MFMA path: WA = plane + E, where the plane
+// (the MFMA operand) holds every entry clamped to [-128, 127] and E the few
+// entries outside it as per-pod lists (row r of the pod array: entries
+// [ptr[r], ptr[r+1]) of (node m, excess e = WA - clamp(WA))).  The cost
+// kernel's epilogue adds e * L[m][n] for the tile's nodes from Lr, a
+// row-major copy of this rank's latency columns (Lr[m][i] = L[m][Nloc0 + i],
+// row stride Mp).  row_pod maps a gathered view's rows to pods (nullptr:
+// row = pod); rows >= *row_count of a view are never read.
+struct Ovf {
+    const int32_t *ptr = nullptr;  // [B * Pp + 1] absolute offsets (nullptr: no entries)
+    const int32_t *m = nullptr;
+    const int32_t *e = nullptr;
+    const signed char *Lr = nullptr;  // [B][N][Mp]
+    const int32_t *row_pod = nullptr;
+    const int32_t *row_count = nullptr;
+    int N = 0;  // rows of one cluster's Lr
+};
+
 }  // namespace nas
 
 struct nas_ctx {
@@ -100,6 +118,12 @@ struct nas_ctx {
     nas::DevBuf host_status; // pinned
     nas::DevBuf ref_stage;   // pinned: nas_score_reference results [P] best | [P][6] winners
     nas::DevBuf scratch;
+    // exact int32 traffic (nas::Ovf): entries outside the int8 plane, and Lr
+    nas::DevBuf ovf_ptr, ovf_m, ovf_e, Lr;
+    int64_t ovf_n = 0;          // entries (0: the plane is the traffic)
+    bool lr_valid = false;      // Lr matches the uploaded latency
+    int64_t wa_abs_row_max = 0; // max over pods of sum_m |WA[p,m]| (int8 path)
+    int32_t L_abs_max = 0;      // max |L| (int8 path)
     bool scored = false;        // a scoring pass filled cand_key
     bool synth_valid = false;   // inputs came from nas_synth_cluster(synth_seed)
     uint64_t synth_seed = 0;
@@ -115,6 +139,12 @@ struct nas_ctx {
     // a G-GPU pass on a single GPU; placements are not meaningful
     int32_t rehearse = 0;
     bool virtual_shard = false;  // nas_set_shard: shard geometry, no exchange
+    // options (nas_set_option)
+    bool opt_stage_timings = true;
+    int64_t opt_comm_timeout_ms = 120000;
+    int32_t opt_rehearse_world = 0;
+    int64_t opt_inject_stall_ms = 0;
+    bool poisoned = false;       // a collective missed its deadline: communicators aborted
     // timing events, created once and reused by every call (hipEventCreate
     // per mark cost a small placement more than its kernels)
     std::vector<hipEvent_t> ev_pool;
@@ -173,7 +203,7 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base,
-                            const Dyn *dyn = nullptr, int batch = 1);
+                            const Dyn *dyn = nullptr, int batch = 1, const Ovf *ovf = nullptr);
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,
@@ -210,8 +240,24 @@ hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap,
 hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *buf, size_t n, int G, int N);
 hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
                               int nloc, int Mp, int Kp, void *Lt);
-hipError_t launch_csr_aggregate(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
-                                const void *w, int dtype, int P, int N, int Kp, void *WA);
+// bf16 CSR traffic -> dense WA rows (fp32 sums, rounded once)
+hipError_t launch_csr_aggregate_bf16(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
+                                     const uint16_t *w, int P, int N, int Kp, uint16_t *WA);
+// int8 plane entries WA[p][m] = v for host-aggregated (pod, node, value) triples
+hipError_t launch_plane_scatter(hipStream_t st, const int32_t *pod, const int32_t *node,
+                                const signed char *val, int64_t n, int Kp, signed char *WA);
+// Lr[m][i] = Lt[i][m] for m < N, i < Mp (one cluster)
+hipError_t launch_make_lr(hipStream_t st, const signed char *Lt, int N, int Mp, int Kp,
+                          signed char *Lr);
+// *out = max(*out, max_r sum_k |WA[r][k]| + sum of |plane + e| - |plane| over r's overflow
+// entries) for rows [0, rows): the exact sum_m |WA[p,m]| (out zeroed by the caller)
+hipError_t launch_row_abs_max(hipStream_t st, const signed char *WA, int64_t rows, int Kp,
+                              const int32_t *ovf_ptr, const int32_t *ovf_m, const int32_t *ovf_e,
+                              unsigned long long *out);
+// *out = max(*out, max |Lt|) (out zeroed by the caller)
+hipError_t launch_abs_max_i8(hipStream_t st, const signed char *a, int64_t n, unsigned *out);
+// a device-side delay of `ms` milliseconds on st (NAS_OPT_INJECT_STALL_MS)
+hipError_t launch_stall(hipStream_t st, int64_t ms);
 
 // nodes [lo, lo + nl) of an n-node synthetic snapshot set, row stride ns
 hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int lo, int nl,
@@ -220,5 +266,12 @@ hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int lo, 
 hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
                                 int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
                                 int32_t *cap, int32_t *req, void *L_full /* optional N*N */);
+// int8 synthetic traffic is exact: pass 0 writes the plane and ovf_cnt[p] (the
+// entries of pod p outside [-128, 127]); pass 1 (after the host's prefix sum
+// into ovf_ptr) writes the entries.  Peer aggregates are recomputed from the
+// seed in both passes, so nothing else is kept between them.
+hipError_t launch_synth_overflow(hipStream_t st, uint64_t seed, int N, int P, int peers, int Kp,
+                                 int pass, const signed char *WA, int32_t *ovf_cnt,
+                                 const int32_t *ovf_ptr, int32_t *ovf_m, int32_t *ovf_e);
 
 }  // namespace nas

@@ -44,7 +44,12 @@ int main(int argc, char **argv) {
                       {"top4/phased/g8", KV(0, 0, 4, 8)}, {"top4/phased/g2", KV(0, 0, 4, 2)},
                       {"top4/touch2", KV(0, 0, 5, 4)}, {"top4/touch3", KV(0, 0, 6, 4)},
                       {"top4/touchB2", KV(0, 0, 7, 4)}, {"noepi/touch2", KV(1, 0, 5, 4)},
-                      {"top4sel/jit", KV(6, 0, 0, 4)}};
+                      {"top4sel/jit", KV(6, 0, 0, 4)},
+#define KV2(E, S, G) (const void *)&k_cost_topk2<NAS_DT_I8, E, S, G>, (S) * TILE_BYTES
+                      {"v2/top4/st4", KV2(0, 4, 4)}, {"v2/noepi/st4", KV2(1, 4, 4)},
+                      {"v2/l2hot", KV2(3, 4, 4)}, {"v2/ldsonly", KV2(4, 4, 4)},
+                      {"v2/top4/st3", KV2(0, 3, 4)}, {"v2/top4/g8", KV2(0, 4, 8)},
+                      {"v2/noepi/st3", KV2(1, 3, 4)}};
     const int nv = sizeof(vars) / sizeof(vars[0]);
     for (int v = 0; v < nv; ++v)
         CK(hipFuncSetAttribute(vars[v].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[v].lds));
@@ -58,11 +63,12 @@ int main(int argc, char **argv) {
     u64 *pa = (u64 *)partial, *pb = (u64 *)pbound;
     int zero = 0;
     const int *nodyn = nullptr;
+    Ovf noovf{};
     for (int r = 0; r < reps; ++r) {
         for (int v = 0; v < nv; ++v) {
-            if (!strchr(vsel, 'a' + v)) continue;
+            if (!strchr(vsel, v < 26 ? 'a' + v : 'A' + v - 26)) continue;
             void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero,
-                            (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero, &nodyn};
+                            (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf};
             CK(hipEventRecord(a));
             CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(THREADS), args, vars[v].lds, 0));
             CK(hipEventRecord(b));

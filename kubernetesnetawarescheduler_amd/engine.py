@@ -53,6 +53,13 @@ class Engine:
     def __exit__(self, *a):
         self.close()
 
+    def set_option(self, key, value):
+        """nas_set_option: key is an NAS_OPT_* constant of _lib (or its name
+        without the prefix, e.g. "STAGE_TIMINGS")."""
+        if isinstance(key, str):
+            key = getattr(_lib, "NAS_OPT_" + key)
+        self._ck(self._L.nas_set_option(self._h, key, int(value)))
+
     def timings(self):
         t = _lib.NasTimings()
         self._ck(self._L.nas_get_timings(self._h, ctypes.byref(t)))
@@ -244,20 +251,41 @@ class Engine:
         self._ck(self._L.nas_upload_pods(self._h, *[ptr(c) for c in cols], req.shape[-2]))
         self.n_pods = req.shape[-2]
 
+    @staticmethod
+    def _int_traffic(a):
+        """Integer traffic for int8 scoring: an int8 array as is (NAS_DT_I8),
+        any other integer array as exact int32 (NAS_DT_I32; never saturated)."""
+        a = np.asarray(a)
+        if a.dtype == np.int8:
+            return as_c(a, np.int8), _lib.NAS_DT_I8
+        if a.dtype.kind not in "iu":
+            raise TypeError("int8 scoring takes integer traffic")
+        if a.size and (a.min() < -2**31 or a.max() > 2**31 - 1):
+            raise ValueError("traffic outside int32")
+        return as_c(a, np.int32), _lib.NAS_DT_I32
+
     def upload_traffic(self, WA, dtype):
-        WA = as_c(WA, self._np(dtype))
+        """dtype "i8": integer traffic (int8 arrays as int8, wider ones as exact
+        int32) against int8 latency; "bf16": bf16 bits."""
+        if dtype in ("i8", "i32"):
+            WA, dt = self._int_traffic(WA)
+        else:
+            WA, dt = as_c(WA, self._np(dtype)), self._dt(dtype)
         P, n = WA.shape[-2:]
-        self._ck(self._L.nas_upload_traffic_dense(self._h, ptr(WA), self._dt(dtype), P, n))
-        self.n_pods, self.n_nodes, self.dtype = P, n, dtype
+        self._ck(self._L.nas_upload_traffic_dense(self._h, ptr(WA), dt, P, n))
+        self.n_pods, self.n_nodes, self.dtype = P, n, "bf16" if dtype == "bf16" else "i8"
 
     def upload_traffic_csr(self, row_ptr, peer_node, weight, dtype, n):
         rp = as_c(row_ptr, np.int32)
         pn = as_c(peer_node, np.int32)
-        w = as_c(weight, self._np(dtype))
+        if dtype in ("i8", "i32"):
+            w, dt = self._int_traffic(weight)
+        else:
+            w, dt = as_c(weight, self._np(dtype)), self._dt(dtype)
         P = rp.shape[0] - 1
-        self._ck(self._L.nas_upload_traffic_csr(self._h, ptr(rp), ptr(pn), ptr(w), self._dt(dtype),
+        self._ck(self._L.nas_upload_traffic_csr(self._h, ptr(rp), ptr(pn), ptr(w), dt,
                                                 P, n, pn.shape[0]))
-        self.n_pods, self.n_nodes, self.dtype = P, n, dtype
+        self.n_pods, self.n_nodes, self.dtype = P, n, "bf16" if dtype == "bf16" else "i8"
 
     def filter(self):
         chunks = (self.n_nodes + 63) // 64
@@ -306,9 +334,11 @@ class Engine:
         self.n_nodes, self.n_pods, self.dtype = n_nodes, P, dtype
 
     def read_inputs(self, p0=0, np_=0, want_L=True):
+        """-> (WA rows [p0, p0+np_) -- exact int32 traffic for int8 scoring,
+        bf16 bits otherwise --, L, capacity (n, 3), requests (P, 3))."""
         n, P = self.n_nodes, self.n_pods
         dt = self._np(self.dtype)
-        WA = np.empty((np_, n), dt) if np_ else None
+        WA = np.empty((np_, n), np.int32 if self.dtype == "i8" else dt) if np_ else None
         L = np.empty((n, n), dt) if want_L else None
         cap = [np.empty(n, np.int32) for _ in range(3)]
         req = [np.empty(P, np.int32) for _ in range(3)]

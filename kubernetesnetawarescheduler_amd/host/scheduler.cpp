@@ -219,7 +219,7 @@ std::vector<std::pair<Pod, Outcome>> CustomScheduler::place_pending(int dtype) {
         if (!api_.node_capacity(nodes[i], cc[i], cm[i], cp[i]))
             throw std::runtime_error("no capacity for node " + nodes[i]);
     std::vector<int32_t> rc(P), rm(P), rp(P, 1), row_ptr(P + 1, 0), peer_node;
-    std::vector<int8_t> weight;
+    std::vector<int32_t> weight;  // exact: aggregated per node in int64 by the engine
     for (int p = 0; p < P; ++p) {
         rc[p] = pods[p].cpu_milli;
         rm[p] = pods[p].mem_kib;
@@ -227,14 +227,14 @@ std::vector<std::pair<Pod, Outcome>> CustomScheduler::place_pending(int dtype) {
             const std::string where = api_.pod_node(q.pod);
             auto it = node_idx.find(where);
             peer_node.push_back(it == node_idx.end() ? -1 : it->second);  // unbound: skipped
-            weight.push_back((int8_t)std::max(-128, std::min(127, q.weight)));
+            weight.push_back(q.weight);
         }
         row_ptr[p + 1] = (int32_t)peer_node.size();
     }
     check(ctx_, nas_upload_latency(ctx_, L.data(), NAS_DT_I8, n), "nas_upload_latency");
     check(ctx_, nas_upload_capacity(ctx_, cc.data(), cm.data(), cp.data(), n), "nas_upload_capacity");
     check(ctx_, nas_upload_pods(ctx_, rc.data(), rm.data(), rp.data(), P), "nas_upload_pods");
-    check(ctx_, nas_upload_traffic_csr(ctx_, row_ptr.data(), peer_node.data(), weight.data(), NAS_DT_I8,
+    check(ctx_, nas_upload_traffic_csr(ctx_, row_ptr.data(), peer_node.data(), weight.data(), NAS_DT_I32,
                                        P, n, (int64_t)peer_node.size()),
           "nas_upload_traffic_csr");
     std::vector<int32_t> node_out(P);

@@ -41,7 +41,7 @@ constexpr size_t kQueueCap = 300;                              // make(chan *v1.
 
 struct Peer {
     std::string pod;  // "namespace/name" of a peer pod
-    int weight;       // traffic volume (MB); int8 range for the int8 engine
+    int weight;       // traffic volume (MB), any int32 (aggregated exactly)
 };
 
 // the fields of *v1.Pod the scheduler reads

@@ -64,9 +64,12 @@ def c2_cluster(seed=0x4E4153, N=1000, P=10000, peers=8, bound_frac=0.2):
 
 
 def csr_to_dense(row_ptr, peer_node, weight, N):
-    """The dense WA the engine aggregates (int8, saturated) -- for oracle checks."""
+    """The dense traffic WA[p, m] = sum of p's weights to peers bound on node m,
+    exact (int64 sums, no saturation; unbound peers, node -1, are skipped) --
+    for oracle checks."""
     P = len(row_ptr) - 1
-    WA = np.zeros((P, N), np.int32)
+    WA = np.zeros((P, N), np.int64)
     rows = np.repeat(np.arange(P), np.diff(row_ptr))
-    np.add.at(WA, (rows, peer_node), weight.astype(np.int32))
-    return np.clip(WA, -128, 127).astype(np.int8)
+    keep = (peer_node >= 0) & (peer_node < N)
+    np.add.at(WA, (rows[keep], peer_node[keep]), np.asarray(weight)[keep].astype(np.int64))
+    return WA

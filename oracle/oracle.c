@@ -28,8 +28,9 @@
  *  (2) EXTENDED MODE -- build-defined (no reference counterpart; parity vs
  *      the reference is "unpinned"):
  *        fit      req[p,r] <= free[n,r] for every resource r
- *        cost     cost[p,n] = sum_m WA[p,m] * L[m,n]   (int64 for int8
- *                 inputs, exact; double for bf16 inputs)
+ *        cost     cost[p,n] = sum_m WA[p,m] * L[m,n]   (int64, exact, for
+ *                 int8 latency with int32 traffic -- the aggregated traffic is
+ *                 never saturated; double for bf16 inputs)
  *        choose   argmin over fitting n of (cost, n) lexicographic
  *        commit   sequential greedy in pod order, free[n] -= req[p]
  *
@@ -245,8 +246,8 @@ void or_fit(int P, int N, const int32_t *rc, const int32_t *rm, const int32_t *r
     }
 }
 
-/* one cost row, int8 inputs: exact int64 */
-static void cost_row_i8(int N, const int8_t *wa_row, const int8_t *L, int64_t *out) {
+/* one cost row, int32 traffic x int8 latency: exact int64 */
+static void cost_row_i8(int N, const int32_t *wa_row, const int8_t *L, int64_t *out) {
     for (int n = 0; n < N; ++n) out[n] = 0;
     for (int m = 0; m < N; ++m) {
         int64_t w = wa_row[m];
@@ -267,7 +268,7 @@ static void cost_row_bf16(int N, const uint16_t *wa_row, const uint16_t *L, doub
     }
 }
 
-void or_cost_i8(int P, int N, const int8_t *WA, const int8_t *L, int64_t *cost) {
+void or_cost_i8(int P, int N, const int32_t *WA, const int8_t *L, int64_t *cost) {
 #pragma omp parallel for schedule(dynamic, 4)
     for (int p = 0; p < P; ++p) cost_row_i8(N, WA + (size_t)p * N, L, cost + (size_t)p * N);
 }
@@ -328,7 +329,8 @@ void or_topk(int P, int N, int k, const int64_t *cost_i, const double *cost_d,
  * Sequential greedy placement, the extended-mode oracle proper.  free_* are
  * updated in place.  Cost rows are computed in parallel blocks (they do not
  * depend on capacity); the commit walk is strictly sequential in pod order.
- * dtype: 1 = int8 (exact int64 costs), 2 = bf16 (double costs).
+ * dtype: 1 = int32 traffic x int8 latency (exact int64 costs), 2 = bf16
+ * (double costs).
  */
 int or_place(int P, int N, int dtype, const void *WA, const void *L, const int32_t *rc,
              const int32_t *rm, const int32_t *rp, int32_t *fc, int32_t *fm, int32_t *fp,
@@ -343,7 +345,7 @@ int or_place(int P, int N, int dtype, const void *WA, const void *L, const int32
         int nb = P - p0 < B ? P - p0 : B;
 #pragma omp parallel for schedule(dynamic, 1)
         for (int i = 0; i < nb; ++i) {
-            if (ci) cost_row_i8(N, (const int8_t *)WA + (size_t)(p0 + i) * N, (const int8_t *)L,
+            if (ci) cost_row_i8(N, (const int32_t *)WA + (size_t)(p0 + i) * N, (const int8_t *)L,
                                 ci + (size_t)i * N);
             else cost_row_bf16(N, (const uint16_t *)WA + (size_t)(p0 + i) * N,
                                (const uint16_t *)L, cd + (size_t)i * N);

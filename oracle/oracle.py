@@ -106,12 +106,21 @@ def fit_mask(req, free):
     return mask
 
 
+def _i32(WA):
+    """Exact integer traffic as int32 (refuses values outside int32)."""
+    a = np.asarray(WA)
+    if a.dtype.kind in "iu" and a.size and (a.min() < -2**31 or a.max() > 2**31 - 1):
+        raise ValueError("traffic outside int32")
+    return _c(a, np.int32)
+
+
 def cost(WA, L, dtype):
-    """dtype 'i8': int8 inputs -> exact int64; 'bf16': uint16 bf16 bits -> float64."""
+    """dtype 'i8': integer traffic (any int32, never saturated) x int8 latency
+    -> exact int64; 'bf16': uint16 bf16 bits -> float64."""
     P, N = WA.shape
     if dtype == "i8":
         out = np.zeros((P, N), np.int64)
-        lib().or_cost_i8(P, N, _ptr(_c(WA, np.int8)), _ptr(_c(L, np.int8)), _ptr(out))
+        lib().or_cost_i8(P, N, _ptr(_i32(WA)), _ptr(_c(L, np.int8)), _ptr(out))
     else:
         out = np.zeros((P, N), np.float64)
         lib().or_cost_bf16(P, N, _ptr(_c(WA, np.uint16)), _ptr(_c(L, np.uint16)), _ptr(out))
@@ -143,7 +152,7 @@ def place(WA, L, req, free, dtype):
     fcols = [np.ascontiguousarray(free[:, i]) for i in range(3)]
     node = np.zeros(P, np.int32)
     if dtype == "i8":
-        dt, wa, ll = 1, _c(WA, np.int8), _c(L, np.int8)
+        dt, wa, ll = 1, _i32(WA), _c(L, np.int8)
         ci = np.zeros(P, np.int64)
         cd = None
     else:

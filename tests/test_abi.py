@@ -37,7 +37,7 @@ def test_binding_covers_header():
 
 
 def test_version():
-    assert _lib.lib().nas_version() == 1
+    assert _lib.lib().nas_version() == 2
 
 
 def test_create_fails_loudly_without_gpu():

@@ -1,0 +1,64 @@
+"""RCCL path hardening (include/nas.h NAS_OPT_COMM_TIMEOUT_MS): a call that
+issued collectives waits under a deadline; on expiry the communicators are
+aborted, the call returns NAS_ERR_COMM and the context is poisoned.  Tested
+at world 1 with an injected device-side stall (NAS_OPT_INJECT_STALL_MS) in
+front of the pass -- the stand-in for a peer rank that never arrives."""
+import numpy as np
+import pytest
+
+from kubernetesnetawarescheduler_amd import Engine, NasError, _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def test_comm_deadline_aborts_and_poisons():
+    with Engine(0) as e:
+        e.comm_init(Engine.comm_unique_id(), 0, 1)
+        e.synth_cluster(7, 512, 2048, "i8", peers=8)
+        node, _, _ = e.place()  # healthy pass through the one-rank communicator
+        assert (node >= -1).all()
+        e.set_option("COMM_TIMEOUT_MS", 200)
+        e.set_option("INJECT_STALL_MS", 1500)
+        with pytest.raises(NasError) as ei:  # (the same pass without the stall succeeds)
+            e.place()
+        assert ei.value.code == _lib.NAS_ERR_COMM
+        assert "did not complete within 200 ms" in str(ei.value)
+        with pytest.raises(NasError) as ei:  # poisoned: every later call fails fast
+            e.reset_capacity()
+        assert ei.value.code == _lib.NAS_ERR_COMM
+    # a fresh context on the same device is unaffected
+    with Engine(0) as e:
+        e.synth_cluster(7, 512, 2048, "i8", peers=8)
+        e.place()
+
+
+def test_comm_deadline_not_hit_when_healthy():
+    with Engine(0) as e:
+        e.comm_init(Engine.comm_unique_id(), 0, 1)
+        e.set_option("COMM_TIMEOUT_MS", 5000)
+        e.set_option("INJECT_STALL_MS", 100)  # shorter than the deadline: just slower
+        e.synth_cluster(8, 512, 2048, "i8", peers=8)
+        a, _, _ = e.place()
+        e.reset_capacity()
+        b, _, _ = e.place()
+        assert (a == b).all()
+
+
+def test_options_reject_bad_values():
+    with Engine(0) as e:
+        for key, val in (("STAGE_TIMINGS", 2), ("COMM_TIMEOUT_MS", -1), ("INJECT_STALL_MS", -5)):
+            with pytest.raises(NasError) as ei:
+                e.set_option(key, val)
+            assert ei.value.code == _lib.NAS_ERR_ARG
+        with pytest.raises(NasError):
+            e.set_option(99, 1)
+        e.set_option("STAGE_TIMINGS", 0)
+        e.synth_cluster(9, 256, 1024, "i8", peers=8)
+        e.place()
+        t = e.timings()
+        assert t["total_ms"] > 0 and t["cost_ms"] == 0  # only the synchronising events
+        e.set_option("STAGE_TIMINGS", 1)
+        e.reset_capacity()
+        e.place()
+        assert e.timings()["cost_ms"] > 0
+    assert np.int32(_lib.NAS_OPT_REHEARSE_WORLD) == 3

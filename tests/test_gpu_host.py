@@ -130,7 +130,7 @@ def test_place_pending_matches_oracle():
     cl = H.FakeCluster(nodes=nodes, capacity=cap, bound=dict(bound))
     pods = []
     for p in range(P):
-        peers = [(f"ns/srv{int(rng.integers(0, 30))}", int(rng.integers(1, 60)))
+        peers = [(f"ns/srv{int(rng.integers(0, 30))}", int(rng.integers(1, 400)))
                  for _ in range(int(rng.integers(0, 5)))]
         peers.append((f"ns/pending{p}", 9))  # an unbound peer is skipped
         pods.append((f"p{p}", int(rng.integers(1, 540)), int(rng.integers(7_464, 303_749)), peers))
@@ -145,7 +145,7 @@ def test_place_pending_matches_oracle():
         for q, w in peers:
             if q in bound:
                 WA[p, nodes.index(bound[q])] += w
-    WA = WA.clip(-128, 127).astype(np.int8)
+    assert WA.max() > 127  # aggregates beyond int8: exact int32 traffic, never saturated
     free = np.array([cap[nd] for nd in nodes], np.int32)
     req = np.array([[c, m, 1] for _, c, m, _ in pods], np.int32)
     want, _, _ = oracle.place(WA, L, req, free, "i8")

@@ -156,7 +156,7 @@ def test_csr_traffic_matches_dense(engine):
         for x in range(row_ptr[p], row_ptr[p + 1]):
             if peer[x] >= 0:
                 dense[p, peer[x]] += w[x]
-    dense = np.clip(dense, -128, 127).astype(np.int8)
+    assert dense.max() > 127  # repeated nodes aggregate past int8: exact, never saturated
     engine.upload_latency(L, "i8")
     engine.upload_capacity(free)
     engine.upload_pods(req)

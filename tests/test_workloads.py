@@ -31,12 +31,13 @@ def test_c2_shape_and_determinism():
     assert (a["req"][:, 2] == 1).all()
 
 
-def test_csr_to_dense_saturates():
-    rp = np.array([0, 3], np.int32)
-    pn = np.array([1, 1, 2], np.int32)
-    w = np.array([100, 100, 5], np.int8)
+def test_csr_to_dense_is_exact():
+    """Aggregated traffic is never saturated (north_star cost = sum_q W[p,q] L[node(q), n])."""
+    rp = np.array([0, 4], np.int32)
+    pn = np.array([1, 1, 2, -1], np.int32)  # -1: unbound peer, skipped
+    w = np.array([100, 100, 5, 77], np.int8)
     WA = workloads.csr_to_dense(rp, pn, w, 4)
-    assert WA.tolist() == [[0, 127, 5, 0]]
+    assert WA.tolist() == [[0, 200, 5, 0]]
 
 
 def test_c2_oracle_places_everything():

@@ -25,7 +25,7 @@ def main():
     a = ap.parse_args()
     e = Engine(0)
     if a.rehearse_world > 1:
-        os.environ["NAS_REHEARSE_WORLD"] = str(a.rehearse_world)
+        e.set_option("REHEARSE_WORLD", a.rehearse_world)
         e.comm_init(Engine.comm_unique_id(), 0, 1)
     e.synth_cluster(0x4E4153, a.nodes, a.pods, "i8")
     if a.rehearse_world > 1:
