@@ -31,13 +31,6 @@ PEAK_I8_TOPS = 5033.2     # dense int8 MFMA, 256 CU x 4 SIMD x 2048 op/clk x 2.4
 PEAK_BF16_TFLOPS = 2516.6  # dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0      # HBM3E spec (MI355X_MICROARCH.md)
 SEED = 0x4E4153
-# HBM-side bytes per launch from rocprofv3 PMC passes (tools/prof_bench.sh ->
-# profiles/r01_s15_prof_summary.json; 16.8-18.6 GB across this round's
-# profiling boxes for k_cost_topk, as Infinity-Cache hits vary): FETCH_SIZE x 2 (gfx950 correction,
-# MI355X_MICROARCH.md) + WRITE_SIZE, for the default workload on one GPU only;
-# any other (kernel, dtype, nodes, pods, world) reports null.
-PMC_TRAFFIC = {("k_cost_topk", "i8", 10000, 100000, 1): 17630158848.0,
-               ("k_vote", "i8", 10000, 100000, 1): 48088230400.0}
 
 
 def parse():
@@ -67,9 +60,82 @@ def parse():
                     help="diagnostic at --gpus 1: time rank 0 of a G-GPU node-sharded pass "
                          "(its node columns; the other ranks' lists are shifted copies of its "
                          "own; placements not meaningful, RCCL over a one-rank communicator)")
-    ap.add_argument("--only", choices=["place", "vote", "score"], default=None,
-                    help="profile helper: run only one path")
+    ap.add_argument("--only", choices=["place", "vote", "score", "pmc"], default=None,
+                    help="profile helper: run only one path (pmc: the score and vote legs, "
+                         "what the in-run PMC passes profile)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the in-run rocprofv3 PMC passes (roofline.traffic then null)")
     return ap.parse_args()
+
+
+def cpu_info():
+    """Host CPU model and the cores this process may use (for the CPU baselines)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"model": model, "nproc": os.cpu_count(), "usable": usable}
+
+
+def pmc_traffic(args):
+    """HBM-side bytes per launch of the dominant kernels, measured in this run:
+    two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: they do not fit one
+    pass on gfx950) over a child `bench.py --only pmc` of the same workload,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 note.  Runs BEFORE this
+    process touches the GPU (the child is a separate process).  Returns
+    {kernel: {"fetch": B, "write": B, "bytes": B}} or {} (with the reason)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return {}, "rocprofv3 not found"
+    child = [sys.executable, os.path.abspath(__file__), "--only", "pmc", "--steps", "1",
+             "--warmup", "0", "--no-pmc", "--nodes", str(args.nodes), "--pods", str(args.pods),
+             "--dtype", args.dtype, "--peers", str(args.peers)]
+    out = {}
+    tmp = tempfile.mkdtemp(prefix="nas_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr)
+            r = subprocess.run(["timeout", "-s", "KILL", "150", prof, "--pmc", ctr,
+                                "--output-format", "csv", "-d", d, "-o", "p", "--"] + child,
+                               cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL)
+            if r.returncode != 0:
+                return {}, f"rocprofv3 --pmc {ctr} exited {r.returncode}"
+            per = {}
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if row["Counter_Name"] != ctr:
+                            continue
+                        k = row["Kernel_Name"].replace("(anonymous namespace)", "").split("(")[0]
+                        k = k.split("<")[0].split("::")[-1].replace("void ", "").strip()
+                        key = (k, row["Dispatch_Id"])
+                        per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+            mult = 2.0 if ctr == "FETCH_SIZE" else 1.0
+            for (k, _), kb in per.items():
+                rec = out.setdefault(k, {})
+                name = "fetch" if ctr == "FETCH_SIZE" else "write"
+                rec[name] = max(rec.get(name, 0.0), kb * 1024.0 * mult)  # the largest dispatch
+        for rec in out.values():
+            rec["bytes"] = rec.get("fetch", 0.0) + rec.get("write", 0.0)
+        return out, None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 class Dist:
@@ -273,9 +339,29 @@ def cpu_baseline_vote(args, eng, ref):
         if t_total > args.cpu_budget_s / 2:
             break
     out = {"value": done * N / t_total, "unit": "pair-scores/s", "cores": 1, "kind": "port",
-           "sample": f"oracle or_vote_literal (C restatement of scheduler.go:250-394, one "
-                     f"thread like wait.Until(Schedule)) on {done} sampled snapshots x {N} nodes",
-           "gpu_matches_oracle_on_sample": bool(ok)}
+           "sample": f"oracle or_vote_literal (C restatement of scheduler.go:250-394 over plain "
+                     f"arrays, one thread like wait.Until(Schedule)) on {done} sampled snapshots "
+                     f"x {N} nodes",
+           "gpu_matches_oracle_on_sample": bool(ok), "cpu": cpu_info()}
+    # the same loop over Go-style maps (oracle/gomap.cpp): nodeMetricsMap
+    # filled per pod (:281-331 minus the scrape), range loops over unordered
+    # maps (:334-394); the GPU is checked on the map orders it walked
+    S_g = min(64, eng.snap_count)
+    snaps = [eng.read_snapshot(s) for s in range(S_g)]
+    batch = {k: np.stack([x[k] for x in snaps]) for k in snaps[0]}
+    del snaps
+    b_g, o1_g, o2_g, (fill_ns, loop_ns) = oracle.vote_gomap(batch)
+    eng.upload_pod_orders(o1_g, o2_g)  # pod p: snapshot p with its own walked orders
+    best_g, _ = eng.score_reference(S_g, pod_snapshot=np.arange(S_g, dtype=np.int32))
+    eng.upload_orders(o1, o2)
+    tot = (fill_ns + loop_ns) * 1e-9
+    out["go_maps"] = {"value": S_g * N / tot, "unit": "pair-scores/s", "cores": 1,
+                      "loop_only_value": S_g * N / (loop_ns * 1e-9),
+                      "sample": f"oracle/gomap.cpp: {S_g} snapshots x {N} nodes, "
+                                f"std::unordered_map<std::string, ...> for nodeMetricsMap and "
+                                f"nodePriorities, map fill {fill_ns * 1e-6:.1f} ms + loops "
+                                f"{loop_ns * 1e-6:.1f} ms",
+                      "gpu_matches_oracle_on_sample": bool((best_g == b_g).all())}
     # the same loop pods-parallel over the host's cores (BASELINE.md plan)
     threads = min(16, os.cpu_count() or 1)
     os.environ["OMP_NUM_THREADS"] = str(threads)
@@ -321,9 +407,28 @@ def config_c1(args, d, eng):
     t = time_steps(d, lambda: eng.score_reference(S), args.steps, args.warmup)
     best, win = eng.score_reference(S)
     ok = True
+    snaps = [eng.read_snapshot(s) for s in range(S)]
     for s in range(S):
-        b, w, _ = oracle.vote(eng.read_snapshot(s), o1, o2)
+        b, w, _ = oracle.vote(snaps[s], o1, o2)
         ok &= b == best[s] and list(w) == win[s].tolist()
+    # configs[0] IS "the reference Go scheduler on CPU": its per-pod loop over
+    # Go-style maps (oracle/gomap.cpp, one thread like wait.Until(Schedule)),
+    # timed on the same 100 snapshots, and the GPU checked on the map orders
+    # that run walked
+    batch = {k: np.stack([x[k] for x in snaps]) for k in snaps[0]}
+    reps, fill, loop = 0, 0, 0
+    t_end = time.perf_counter() + 2.0
+    while time.perf_counter() < t_end:
+        b_g, o1_g, o2_g, (f_ns, l_ns) = oracle.vote_gomap(batch)
+        fill, loop, reps = fill + f_ns, loop + l_ns, reps + 1
+    eng.upload_orders(o1_g, o2_g)
+    best_g, _ = eng.score_reference(S)
+    cpu_ms = (fill + loop) * 1e-6 / reps
+    cpu_base = {"value": S * N / (cpu_ms * 1e-3), "unit": "pair-scores/s", "cores": 1,
+                "kind": "port", "ms_per_step": cpu_ms, "loop_only_ms": loop * 1e-6 / reps,
+                "sample": f"oracle/gomap.cpp (scheduler.go:281-394 over std::unordered_map, "
+                          f"map fill + loops), the same {S} snapshots, {reps} repetitions",
+                "gpu_matches_on_its_map_orders": bool((best_g == b_g).all()), "cpu": cpu_info()}
     # extended mode on the same shape: every pod sends
     # 100 MB (customNetworkBenchmark/*.data:2) to one bound server pod, seeded
     # 10 x 10 int8 latency, Raspberry-Pi-sized capacity
@@ -347,8 +452,12 @@ def config_c1(args, d, eng):
                         f"extended mode on the same shape (100 MB per pod to one server pod)",
             "value": S * N / (t / args.steps), "unit": "pair-scores/s",
             "ms_per_step": t * 1e3 / args.steps, "matches_oracle": bool(ok),
+            "cpu_baseline": cpu_base,
             "extended": {"ms_per_step": te * 1e3 / args.steps,
                          "placements_per_s": P / (te / args.steps), "matches_oracle": bool(ok_ext)},
+            "bound": "latency: one nas_score_reference call (a few tens of microseconds of launch "
+                     "and copy; 48 KB of snapshots) per step -- the HBM or MFMA roofline does not "
+                     "apply at 1000 pairs",
             "note": "launch-latency bound: one score_reference / nas_place call per step"}
 
 
@@ -364,16 +473,30 @@ def config_c2(args, d, eng):
     eng.upload_pods(c["req"])
     eng.upload_traffic_csr(c["row_ptr"], c["peer_node"], c["weight"], "i8", N)
     t, res = _timed_place(d, eng, args.steps, args.warmup)
+    stages = {k: res["t"][k] for k in ("fit_ms", "cost_ms", "merge_ms", "commit_ms", "total_ms",
+                                        "rescore_rounds", "rescored_pods", "commit_rounds")}
     WA = workloads.csr_to_dense(c["row_ptr"], c["peer_node"], c["weight"], N)
+    t0 = time.perf_counter()
     want, wcost, wfree = oracle.place(WA, c["L"], c["req"], c["free"], "i8")
+    t_cpu = time.perf_counter() - t0
     ok = (res["node"] == want).all() and (res["score"] == wcost).all() \
         and (eng.get_capacity() == wfree).all()
     ms = t * 1e3 / args.steps
     return {"workload": f"C2: clusterloader2 requests, {N} nodes x {P} pods, CSR traffic "
-                        f"({len(c['peer_node'])} nnz), latency U[50,500] us in 4-us int8 steps",
+                        f"({len(c['peer_node'])} nnz, exact int32 aggregation), latency "
+                        f"U[50,500] us in 4-us int8 steps",
             "value": P * N / (ms * 1e-3), "unit": "pair-scores/s", "ms_per_step": ms,
             "placements_per_s": P / (ms * 1e-3), "unschedulable": res["t"]["unschedulable"],
-            "matches_oracle": bool(ok), "oracle_check": f"all {P} pods, scores and capacity"}
+            "matches_oracle": bool(ok), "oracle_check": f"all {P} pods, scores and capacity",
+            "stages_ms": stages,
+            "bound": "latency: the contraction is 2e10 int8 ops (~4 us at the MFMA peak); a pass "
+                     "is the pipeline's launches plus the commit's stops -- each gathered rescore "
+                     "slot (stale scan, compact, gather, fit, cost, merge, commit) is a chain of "
+                     "dependent small launches (stages_ms: device-side sums)",
+            "cpu_baseline": {"value": P * N / t_cpu, "unit": "pair-scores/s",
+                             "cores": int(os.environ.get("OMP_NUM_THREADS", "1")), "kind": "port",
+                             "ms_per_step": t_cpu * 1e3,
+                             "sample": "oracle/oracle.c or_place on the whole C2 workload"}}
 
 
 def config_c5(args, d, eng, B=64, N=5000, P=5000, sample=1024):
@@ -384,14 +507,33 @@ def config_c5(args, d, eng, B=64, N=5000, P=5000, sample=1024):
     eng.synth_batch(SEED, B, N, P, "i8", peers=args.peers)
     t, res = _timed_place(d, eng, args.steps, args.warmup)
     WA, L, cap, req = eng.read_inputs(0, sample, want_L=True)
+    t0 = time.perf_counter()
     want, wcost, _ = oracle.place(WA, L, req[:sample], cap, "i8")
+    t_cpu = time.perf_counter() - t0
     ok = (res["node"][0, :sample] == want).all() and (res["score"][0, :sample] == wcost).all()
     ms = t * 1e3 / args.steps
+    # roofline of the batched contraction: one k_cost_topk launch over all
+    # clusters (nas_score), HIP events; 2 * B * P * N * N int8 ops
+    eng.reset_capacity()
+    cms = []
+    for _ in range(4):
+        eng.score()
+        cms.append(eng.timings()["cost_ms"])
+    cost_ms = float(np.median(cms[1:]))
+    kpad = -(-N // 128) * 128
+    ops = 2.0 * B * P * N * kpad
     return {"workload": f"C5: batch of {B} clusters x {N} nodes x {P} pods (synthetic, seeded)",
             "value": B * P * N / (ms * 1e-3), "unit": "pair-scores/s", "ms_per_step": ms,
             "placements_per_s": B * P / (ms * 1e-3), "unschedulable": res["t"]["unschedulable"],
             "rescore_rounds": res["t"]["rescore_rounds"], "matches_oracle": bool(ok),
-            "oracle_check": f"cluster 0, first {sample} pods"}
+            "oracle_check": f"cluster 0, first {sample} pods",
+            "roofline": {"kernel": "k_cost_topk (batched, one launch)", "bound": "mfma",
+                         "achieved": ops / (cost_ms * 1e-3) / 1e12, "peak": PEAK_I8_TOPS,
+                         "unit": "TFLOP/s", "frac": ops / (cost_ms * 1e-3) / 1e12 / PEAK_I8_TOPS,
+                         "launch_ms": cost_ms, "ops_per_launch": ops},
+            "cpu_baseline": {"value": sample * N / t_cpu, "unit": "pair-scores/s",
+                             "cores": int(os.environ.get("OMP_NUM_THREADS", "1")), "kind": "port",
+                             "sample": f"oracle or_place on cluster 0's first {sample} pods"}}
 
 
 def config_c4(args, d, eng, N=50000, P=500000):
@@ -433,6 +575,10 @@ def _claim_stdout():
 def main():
     args = parse()
     result_out = _claim_stdout()
+    traffic, traffic_why = {}, "not collected (--no-pmc or a multi-GPU run)"
+    if (not args.no_pmc and args.only is None and args.gpus == 1
+            and int(os.environ.get("WORLD_SIZE", "1")) == 1):
+        traffic, traffic_why = pmc_traffic(args)  # before this process initialises the GPU
     d = Dist(args.gpus)
     from kubernetesnetawarescheduler_amd import Engine
     eng = Engine(d.local)
@@ -452,7 +598,7 @@ def main():
         out["rehearsal"] = (f"rank 0 of a {args.rehearse_world}-GPU node-sharded pass on one GPU: "
                             "its node columns scored, the other ranks' lists stood in for by "
                             "shifted copies; NOT a multi-GPU measurement, placements not checked")
-    if args.only not in ("vote", "score"):
+    if args.only not in ("vote", "score", "pmc"):
         elapsed, per, gpu_nodes = bench_place(args, d, eng)
         out["value"] = P * N / (elapsed / args.steps)
         out["ms_per_step"] = elapsed * 1e3 / args.steps
@@ -465,7 +611,7 @@ def main():
                               "third, so stages overlap")
         out["rescore_rounds"] = per["rescore_rounds"]
         out["unschedulable"] = per["unschedulable"]
-    if args.only != "vote":
+    if args.only not in ("vote",):
         if gpu_nodes is None:
             eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
         cost_ms, samples = bench_cost_kernel(args, d, eng)
@@ -477,12 +623,20 @@ def main():
                            "peak": peak, "unit": "TFLOP/s",
                            "op_type": "int8 ops (2 per MAC) vs the dense int8 MFMA peak"
                                       if args.dtype == "i8" else "bf16 FLOPs",
-                           "frac": achieved / peak, "traffic": PMC_TRAFFIC.get(("k_cost_topk", args.dtype, N, P, d.world)),
+                           "frac": achieved / peak,
+                           "traffic": traffic.get("k_cost_topk", {}).get("bytes"),
                            "traffic_unit": "B/launch",
+                           "traffic_note": ("HBM-side bytes of the largest k_cost_topk dispatch, "
+                                            "rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE in this run"
+                                            if traffic else traffic_why),
                            "launch_ms": cost_ms, "ops_per_launch": ops,
                            "note": "one launch over all pods x this rank's node columns "
                                    "(nas_score), HIP events on its stream; 2*P*N*N_local ops"}
-    if not args.no_reference_mode and args.only in (None, "vote"):
+    if traffic.get("k_fit"):
+        fb = 2.0 * N * 4 * 3 + 2.0 * P * 4 * 3 + P * ((N + 63) // 64) * 8.0  # capacities, requests, mask
+        out["fit_traffic"] = {"kernel": "k_fit", "bytes": traffic["k_fit"]["bytes"],
+                              "algorithmic_bytes": fb, "unit": "B/launch"}
+    if not args.no_reference_mode and args.only in (None, "vote", "pmc"):
         elapsed, vote_ms, S, ref = bench_vote(args, d, eng)
         pods_total = S if args.vote_node_shard else S * d.world
         nloc = (d.rank + 1) * N // d.world - d.rank * N // d.world if args.vote_node_shard else N
@@ -498,9 +652,10 @@ def main():
                          "achieved": bytes_launch / (vote_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s",
                          "frac": bytes_launch / (vote_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                         "traffic": PMC_TRAFFIC.get(("k_vote", args.dtype, N, P, d.world)),
+                         "traffic": traffic.get("k_vote", {}).get("bytes"),
                          "traffic_unit": "B/launch", "launch_ms": vote_ms, "bytes_per_launch": bytes_launch}}
-        if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and not args.vote_node_shard:
+        if (d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and not args.vote_node_shard
+                and args.only != "pmc"):
             out["reference_mode"]["cpu_baseline"] = cpu_baseline_vote(args, eng, ref)
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and gpu_nodes is not None:
         # the vote path freed nothing; re-synthesise the cluster inputs (same seed)

@@ -55,6 +55,9 @@ extern "C" {
 #define NAS_DT_BF16 2 /* bf16 bits (uint16), fp32 accumulation */
 #define NAS_DT_I32 3  /* traffic only, with NAS_DT_I8 latency: int32 traffic, exact integer
                        * scores (see nas_upload_traffic_dense) */
+#define NAS_DT_F32 4  /* fp32 latency and traffic as measured (no quantisation): exact
+                       * fp32 products on v_mfma_f32_32x32x2_f32, fp32 accumulation --
+                       * costs within 1e-5 relative of an fp64 sum */
 
 /* winner slots returned by nas_score_reference (order of scheduler.go:360-365) */
 #define NAS_W_CPU 0
@@ -143,6 +146,14 @@ int nas_upload_snapshot(nas_ctx *ctx, const double *cpu, const double *mem, cons
 int nas_upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
                       int32_t n_orders);
 
+/* One order set per POD instead (n_pods sets): pod p of the next
+ * nas_score_reference (which must score exactly n_pods pods) walks order set
+ * p on snapshot pod_snapshot[p] -- e.g. a batch of pods scored against ONE
+ * scraped snapshot, each pod with the map orders of its own prioritize call
+ * (scheduler.go:334, :387), without a snapshot copy per pod. */
+int nas_upload_pod_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
+                          int32_t n_pods);
+
 /* Score P pods.  order1/order2 non-NULL: one shared order set for this call;
  * NULL: the sets from nas_upload_orders.  pod_snapshot NULL: pod p uses
  * snapshot p.  best_out[P]: node index / NAS_NONE / NAS_EMPTY (the
@@ -212,7 +223,7 @@ int nas_vote_merge(nas_ctx *ctx, const nas_vote_partial *parts, int32_t n_parts,
  */
 
 /* Dense latency matrix L[m * n + j] = latency from node m to node j,
- * uploaded once (dtype NAS_DT_I8 or NAS_DT_BF16).  Integer scores are exact
+ * uploaded once (dtype NAS_DT_I8, NAS_DT_BF16 or NAS_DT_F32).  Integer scores are exact
  * int32: nas_place / nas_score return NAS_ERR_UNSUPPORTED when some pod's
  * sum_m |WA[p,m]| * max|L| exceeds INT32_MAX. */
 int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n);
@@ -237,7 +248,8 @@ int nas_upload_pods(nas_ctx *ctx, const int32_t *req_cpu_milli, const int32_t *r
  * latency's (NAS_DT_I8 / NAS_DT_BF16), or NAS_DT_I32 with NAS_DT_I8 latency --
  * the cost stays the exact sum_m WA[p,m] * L[m,n] for any int32 traffic (the
  * engine keeps an int8 plane for the MFMA and adds the few entries outside
- * [-128, 127] exactly in the contraction's epilogue). */
+ * [-128, 127] exactly in the contraction's epilogue); NAS_DT_F32 with
+ * NAS_DT_F32 latency. */
 int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_t P, int32_t n);
 
 /* Same from a sparse pod-communication graph: for pod p the peers are
@@ -245,7 +257,8 @@ int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_
  * -1 for an unbound peer, which is skipped) with weights weight[...]:
  * int8 (NAS_DT_I8) or int32 (NAS_DT_I32) with int8 latency -- summed exactly
  * (no saturation; an aggregate outside int32 is NAS_ERR_UNSUPPORTED) -- or
- * bf16 bits (NAS_DT_BF16), summed in fp32 on the device and rounded once. */
+ * bf16 bits (NAS_DT_BF16), summed in fp32 on the device and rounded once,
+ * or fp32 (NAS_DT_F32), summed in fp64 on the host and rounded once. */
 int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *peer_node,
                            const void *weight, int32_t dtype, int32_t P, int32_t n,
                            int64_t nnz);

@@ -62,6 +62,12 @@ int nas_host_iperf_receiver(const char *json, size_t n, double *receiver_bps, do
 int nas_host_latency_matrix(int32_t n, const char *const *reports, const size_t *report_len,
                             int8_t *L_out);
 int32_t nas_host_latency_from_bps(double bps);
+/* The unquantised form for NAS_DT_F32 placement: microseconds to move 1 MB
+ * (8e12 / bps) as float, the slower direction of each pair, 0 on the
+ * diagonal; a pair without a usable report costs 1e7 us (never Inf). */
+int nas_host_latency_matrix_us(int32_t n, const char *const *reports, const size_t *report_len,
+                               float *L_out);
+float nas_host_latency_us_from_bps(double bps);
 
 /* ---- the scheduler loop ----------------------------------------------------- */
 
@@ -106,8 +112,13 @@ int nas_host_set_topology(nas_host_sched *s, const char *const *names, const cha
                           int32_t n);
 /* Per-node iperf report paths, replacing the reference's map (:505-510). */
 int nas_host_set_iperf_path(nas_host_sched *s, const char *node, const char *path);
-/* Pairwise latency for the network-aware path, rows/cols named by names[]. */
+/* Pairwise latency for the network-aware path, rows/cols named by names[]:
+ * int8 ms (exact integer scores) or, _f32, measured microseconds (fp32 costs
+ * on NAS_DT_F32; peer weights then enter as float MB).  The latency set last
+ * decides the path of nas_host_place_pending. */
 int nas_host_set_latency(nas_host_sched *s, const char *const *names, const int8_t *L, int32_t n);
+int nas_host_set_latency_f32(nas_host_sched *s, const char *const *names, const float *L,
+                             int32_t n);
 
 typedef struct nas_host_pod {
     const char *ns, *name, *uid, *scheduler_name, *node_name;

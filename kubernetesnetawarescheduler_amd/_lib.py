@@ -23,6 +23,7 @@ NAS_EMPTY = -1
 NAS_DT_I8 = 1
 NAS_DT_BF16 = 2
 NAS_DT_I32 = 3  # traffic only (int8 latency): exact int32 traffic
+NAS_DT_F32 = 4  # fp32 latency and traffic, fp32 MFMA
 NAS_OPT_STAGE_TIMINGS = 1
 NAS_OPT_COMM_TIMEOUT_MS = 2
 NAS_OPT_REHEARSE_WORLD = 3
@@ -77,6 +78,7 @@ SIGNATURES = {
     "nas_set_option": (_I, [_CTX, _I, _c.c_int64]),
     "nas_upload_snapshot": (_I, [_CTX, _V, _V, _V, _V, _V, _V, _I, _I]),
     "nas_upload_orders": (_I, [_CTX, _V, _V, _I]),
+    "nas_upload_pod_orders": (_I, [_CTX, _V, _V, _I]),
     "nas_score_reference": (_I, [_CTX, _V, _V, _V, _I, _V, _V]),
     "nas_upload_snapshot_shard": (_I, [_CTX, _V, _V, _V, _V, _V, _V, _I, _I, _I, _I]),
     "nas_vote_partials": (_I, [_CTX, _V, _V, _I, _V]),

@@ -80,6 +80,27 @@ struct Mma<NAS_DT_I8> {
     static __device__ __forceinline__ unsigned okey(int x) { return (unsigned)x ^ 0x80000000u; }
 };
 
+// fp32: one 16-byte fragment holds 4 k-values per lane; element j of lane
+// half h is k-pair j of the MFMA (any permutation of K works when A and B use
+// the same one), so a fragment pair is 4 v_mfma_f32_32x32x2_f32 -- exact fp32
+// products, fp32 accumulation
+template <>
+struct Mma<NAS_DT_F32> {
+    using acc_t = v16f;
+    static __device__ __forceinline__ acc_t mma(v4i a, v4i b, acc_t c) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            c = __builtin_amdgcn_mfma_f32_32x32x2f32(__int_as_float(a[j]), __int_as_float(b[j]), c,
+                                                     0, 0, 0);
+        return c;
+    }
+    static __device__ __forceinline__ unsigned okey(float x) {
+        x = x + 0.0f;
+        const unsigned u = __float_as_uint(x);
+        return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    }
+};
+
 template <>
 struct Mma<NAS_DT_BF16> {
     using acc_t = v16f;
@@ -734,289 +755,6 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_cost_topk2: the same 256-node x 256-pod workgroup tile with the roles of
-// the operands split by where they are shared.
-//   * Lt (nodes) is shared by every wave: staged once per workgroup into an
-//     LDS ring of NST 32-KiB stages by LDS-DMA (4 pieces per wave per K-step,
-//     half of k_cost_topk's), DMA'd NST-1 K-steps ahead.
-//   * WA (pods) is private: wave w owns pods 32w .. 32w+31 of the tile and
-//     streams its rows straight into registers (global_load_dwordx4, 64
-//     contiguous bytes per lane per K-step), two K-steps ahead -- no LDS
-//     round trip and no LDS-DMA issue cost for the 1-GB operand.
-// A K-step's 128 bytes are split by lane half h: half h contracts bytes
-// [64h, 64h + 64), 16 per k-substep (the contraction order is free; A's
-// fragment reads use the same permutation).  Each wave computes all 256
-// nodes x its 32 pods = 8 MFMA tiles: 8 ds_read_b128 + 8 MFMAs per k-substep.
-// A lane ends with 128 (node, cost) values of ONE pod, so the top-k needs no
-// cross-wave merge: per-lane top-4, one lane^32 exchange, 72 B per pod.
-// ---------------------------------------------------------------------------
-template <int DT, int EPI = 0, int NST = 4, int GM = COST_GM>
-__global__ void __launch_bounds__(THREADS, 1)
-k_cost_topk2(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
-             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
-             u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base,
-             const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
-             Ovf ov) {
-    using M = Mma<DT>;
-    using acc_t = typename M::acc_t;
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-
-    // ---- XCD-aware tile order (speed only), as k_cost_topk
-    const int nwg = n_mt * n_nt;
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int gsize = GM * n_nt;
-    const int g = v / gsize;
-    const int first_mt = g * GM;
-    const int gm = min(n_mt - first_mt, GM);
-    const int mt = first_mt + (v % gsize) % gm;
-    const int nt = (v % gsize) / gm;
-    const int cb = blockIdx.y;
-    Lt += (size_t)cb * n_mt * BM * Kb;
-    WA += (size_t)cb * Pp * Kb;
-    mask += (size_t)cb * (n_mt * BM / 64) * Pp;
-    partial += (size_t)cb * n_mt * Pp * KC;
-    pbound += (size_t)cb * n_mt * Pp;
-    if (dyn_start) {
-        const int s0 = dyn_start[cb * STATUS_INTS];
-        if (s0 < 0) return;
-        if (dyn_hi_ptr) dyn_hi = dyn_hi_ptr[cb * STATUS_INTS];
-        p0 = s0 / BN * BN;
-        if (p0 + nt * BN >= dyn_hi) return;  // whole block: before any barrier
-    }
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int fr = lane & 31, fh = lane >> 5;
-    const int pod_row = p0 + nt * BN + w * 32 + fr;  // this lane's pod (row of WA)
-    const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
-    const unsigned char *Bl = WA + (size_t)pod_row * Kb + 64 * fh;
-    if constexpr (EPI == 3) {  // diagnostic: every block streams tile (0, 0)
-        Ag = Lt;
-        Bl = WA + (size_t)(w * 32 + fr) * Kb + 64 * fh;
-    }
-
-    // LDS-DMA piece j of wave w: rows (8j + w)*8 .. +8 of the stage, whole
-    // 128-B lines, chunk swizzle chunk ^= (row >> 1) & 7 on the SOURCE side
-    const int srow_in = lane >> 3, sq = lane & 7;
-    auto stageA = [&](int buf, int k0) {
-        unsigned char *base = lds + buf * TILE_BYTES;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int r0 = (j * 8 + w) * 8;
-            const int row = r0 + srow_in;
-            const int c = sq ^ ((row >> 1) & 7);
-            glds16(Ag + (size_t)row * Kb + k0 + c * 16, base + r0 * BKB);
-        }
-    };
-    auto loadB = [&](v4i (&b)[4], int k0) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) b[s] = *reinterpret_cast<const v4i *>(Bl + k0 + 16 * s);
-    };
-
-    // the epilogue's fit-mask words (4 per pod: nodes 64c .. 64c+63 of the tile)
-    u64 mw[4];
-    if constexpr (EPI == 0) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) mw[c] = mask[(size_t)(mt * 4 + c) * Pp + pod_row];
-    }
-    acc_t acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = acc_t{};
-    // ---- exact int32 traffic: the pod's entries outside the int8 plane,
-    // e * L[m][n] over the tile's nodes, are the accumulators' initial value
-    // (added before the K loop, while its operand registers are still free)
-    if constexpr (DT == NAS_DT_I8 && EPI == 0) {
-        if (ov.ptr) {
-            const int r = pod_row;
-            int beg = 0, end = 0;
-            if (r < (ov.row_count ? *ov.row_count : 0x7fffffff)) {
-                const int pod = (ov.row_pod ? ov.row_pod[r] : r) + cb * Pp;
-                beg = ov.ptr[pod];
-                end = ov.ptr[pod + 1];
-            }
-            const signed char *lr =
-                ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + 4 * fh;
-            // node tile outermost: one tile's 16 accumulators live in the
-            // entry loop at a time (the whole row at once spills)
-#pragma unroll
-            for (int mi = 0; mi < 8; ++mi)
-                for (int j = beg; j < end; ++j) {
-                    const int e = ov.e[j];
-                    const signed char *row = lr + (size_t)ov.m[j] * (n_mt * BM) + mi * 32;
-#pragma unroll
-                    for (int g4 = 0; g4 < 4; ++g4) {
-                        const int x = *reinterpret_cast<const int *>(row + 8 * g4);
-#pragma unroll
-                        for (int c = 0; c < 4; ++c)
-                            acc[mi][4 * g4 + c] += e * (int)(signed char)(x >> (8 * c));
-                    }
-                }
-        }
-    }
-
-
-    // one K-step from stage `buf` with this wave's B registers
-    auto compute = [&](int buf, const v4i (&b)[4]) {
-        const unsigned char *As = lds + buf * TILE_BYTES;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int c = 4 * fh + s;
-            v4i a[8];
-#pragma unroll
-            for (int mi = 0; mi < 8; ++mi) {
-                const int r = mi * 32 + fr;
-                a[mi] = *reinterpret_cast<const v4i *>(As + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int mi = 0; mi < 8; ++mi) acc[mi] = M::mma(a[mi], b[s], acc[mi]);
-        }
-    };
-
-    const int nk = Kb / BKB;
-    v4i b0[4], b1[4];
-    if constexpr (EPI == 4) {
-        // diagnostic: stage once, then the K loop on LDS + registers only
-        stageA(0, 0);
-        loadB(b0, 0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        for (int t = 0; t < nk; ++t) {
-            compute(0, b0);
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-        }
-    } else {
-        // issue order: A(0) .. A(NST-2), B(0), B(1); step t: [wait A(t), B(t);
-        // barrier] A(t+NST-1), compute t, B(t+2).  At the top of step t >= 1
-        // the ops issued after B(t) are A(t+NST-2) and B(t+1) (each 4
-        // instructions, when they exist): vmcnt(8 / 4 / 0) retires B(t) and,
-        // older still, A(t).
-        for (int t = 0; t < NST - 1; ++t)
-            if (t < nk) stageA(t, t * BKB);
-        loadB(b0, 0);
-        if (nk > 1) loadB(b1, BKB);
-        auto wait_step = [&](int t) {
-            const int n = t == 0 ? (nk > 1 ? 4 : 0)
-                                 : 4 * (t + NST - 2 < nk) + 4 * (t + 1 < nk);
-            if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-            else if (n == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();  // every wave's pieces of A(t) landed;
-            asm volatile("" ::: "memory");  // stage (t-1) % NST is free
-        };
-        // two K-steps per iteration, so the B register buffers have fixed names
-        int t = 0;
-        for (; t + 1 < nk; t += 2) {
-            wait_step(t);
-            if (t + NST - 1 < nk) stageA((t + NST - 1) % NST, (t + NST - 1) * BKB);
-            compute(t % NST, b0);
-            if (t + 2 < nk) loadB(b0, (t + 2) * BKB);
-            wait_step(t + 1);
-            if (t + NST < nk) stageA((t + NST) % NST, (t + NST) * BKB);
-            compute((t + 1) % NST, b1);
-            if (t + 3 < nk) loadB(b1, (t + 3) * BKB);
-        }
-        if (t < nk) {
-            wait_step(t);
-            compute(t % NST, b0);
-        }
-    }
-    if constexpr (EPI != 0) {
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-#if defined(__HIP_DEVICE_COMPILE__)
-            asm volatile("" ::"v"(acc[mi]));
-#endif
-        }
-        return;
-    }
-
-    // ---- epilogue: per lane the top-4 of its pod's 128 (node, cost) values,
-    // merged with lane ^ 32 (the same pod, the other 4 rows of each group)
-    // into the pod's 8-list over the tile's 256 nodes
-    unsigned u[8][16];
-    unsigned kmin = 0xffffffffu, kmax = 0u;
-    int smin = 0x7fffffff, smax = -0x7fffffff - 1;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-            if constexpr (DT == NAS_DT_I8) {
-                smin = min(smin, (int)acc[mi][reg]);
-                smax = max(smax, (int)acc[mi][reg]);
-            } else {
-                u[mi][reg] = M::okey(acc[mi][reg]);
-                kmin = min(kmin, u[mi][reg]);
-                kmax = max(kmax, u[mi][reg]);
-            }
-        }
-    if constexpr (DT == NAS_DT_I8) {
-        kmin = M::okey(smin);
-        kmax = M::okey(smax);
-    }
-    u64 k4[4];
-    const unsigned nb = (unsigned)(node_base + mt * BM + 4 * fh);
-    if (__all(kmax - kmin < (1u << 25) - 1u)) {
-        // packed: (key - kmin) << 7 | i, i = mi * 16 + reg increasing in node
-        // order; a non-fitting value is all-ones.  Sorted insert by med3.
-        unsigned c0 = 0xffffffffu, c1 = c0, c2 = c0, c3 = c0;
-        const unsigned nk7 = 0u - ((DT == NAS_DT_I8 ? (unsigned)smin : kmin) << 7);
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-            const unsigned nbits = ~(unsigned)(mw[mi >> 1] >> (32 * (mi & 1)));
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
-                const unsigned raw = DT == NAS_DT_I8 ? (unsigned)(int)acc[mi][reg] : u[mi][reg];
-                const unsigned x = ((raw << 7) + nk7) | (unsigned)(mi * 16 + reg) |
-                                   (unsigned)__builtin_amdgcn_sbfe((int)nbits, row, 1);
-                c3 = umed3(c2, c3, x);
-                c2 = umed3(c1, c2, x);
-                c1 = umed3(c0, c1, x);
-                c0 = min(c0, x);
-            }
-        }
-        const unsigned cc[4] = {c0, c1, c2, c3};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const unsigned i = cc[j] & 127u, r = i & 15u;
-            const unsigned node = nb + (i >> 4) * 32u + (r & 3u) + 8u * (r >> 2);
-            k4[j] = cc[j] == 0xffffffffu ? KEY_INVALID : ((u64)((cc[j] >> 7) + kmin) << 32) | node;
-        }
-    } else {
-        Top4 t4;
-        t4.init();
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-            const unsigned bits = (unsigned)(mw[mi >> 1] >> (32 * (mi & 1)));
-            const unsigned node0 = nb + mi * 32;
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int row = (reg & 3) + 8 * (reg >> 2);
-                const unsigned key = DT == NAS_DT_I8 ? M::okey(acc[mi][reg]) : u[mi][reg];
-                const unsigned x = key | ((((bits >> (row + 4 * fh)) & 1u) ^ 1u) * 0xffffffffu);
-                t4.insert(x, node0 + row);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) k4[j] = t4.c[j] == 0xffffffffu ? KEY_INVALID : t4.key(j);
-    }
-    u64 o4[4], l8[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o4[j] = shfl_xor64(k4[j], 32);
-    merge44(k4, o4, l8);
-    const u64 bnd = umin64(umin64(k4[3], o4[3]), l8[7]);
-    // both halves hold the same list: half h stores keys 4h .. 4h+3
-    u64 *dst = partial + ((size_t)mt * Pp + pod_row) * KC + 4 * fh;
-    const u64 q0 = fh ? l8[4] : l8[0], q1 = fh ? l8[5] : l8[1];
-    const u64 q2 = fh ? l8[6] : l8[2], q3 = fh ? l8[7] : l8[3];
-    reinterpret_cast<ulonglong2 *>(dst)[0] = make_ulonglong2(q0, q1);
-    reinterpret_cast<ulonglong2 *>(dst)[1] = make_ulonglong2(q2, q3);
-    if (fh == 0) pbound[(size_t)mt * Pp + pod_row] = bnd;
-}
-
 // merge n_lists candidate lists per pod (list l of pod p at
 // keys[l * stride + (p - src_p0) * KC], bound[l * bstride + p - src_p0]).
 // MERGE_LANES lanes per pod: lane s folds lists s, s + MERGE_LANES, ... in
@@ -1088,13 +826,7 @@ NAS_INST(0, 1, 2, 4) NAS_INST(0, 1, 3, 4) NAS_INST(0, 0, 2, 4) NAS_INST(0, 0, 3,
 NAS_INST(1, 1, 2, 4) NAS_INST(1, 1, 3, 4)
 NAS_INST(0, 0, 4, 4) NAS_INST(1, 0, 4, 4) NAS_INST(0, 0, 4, 8) NAS_INST(0, 0, 4, 2)
 #undef NAS_INST
-#define NAS_INST2(E, S, G)                                                                         \
-    template __global__ void k_cost_topk2<NAS_DT_I8, E, S, G>(                                     \
-        const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
-        u64 *, int, const int *, int, const int *, Ovf);
-NAS_INST2(0, 4, 4) NAS_INST2(1, 4, 4) NAS_INST2(3, 4, 4) NAS_INST2(4, 4, 4) NAS_INST2(0, 3, 4)
-NAS_INST2(0, 4, 8) NAS_INST2(1, 3, 4)
-#undef NAS_INST2
+
 #endif
 
 template <int DT>
@@ -1141,6 +873,11 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
         if (Kp % BKB) return hipErrorInvalidValue;
         return launch_cost_t<NAS_DT_I8>(st, Lt, WA, Mp, Kp, Pp, p0, np, mask, partial, pbound,
                                         node_base, dyn, batch, ov);
+    }
+    if (dtype == NAS_DT_F32) {
+        if ((4 * Kp) % BKB) return hipErrorInvalidValue;
+        return launch_cost_t<NAS_DT_F32>(st, Lt, WA, Mp, 4 * Kp, Pp, p0, np, mask, partial, pbound,
+                                         node_base, dyn, batch, Ovf{});
     }
     if ((2 * Kp) % BKB) return hipErrorInvalidValue;
     return launch_cost_t<NAS_DT_BF16>(st, Lt, WA, Mp, 2 * Kp, Pp, p0, np, mask, partial, pbound,

@@ -14,8 +14,13 @@
 // group's result, so 64 pods end in one coalesced 8-byte-per-lane store:
 //   mask[c * Pp + p]  bit j  <=>  pod p fits local node 64c + j.
 // ~8 instructions per (pod, 64 nodes) instead of ~6 per (pod, node) in a
-// lane-per-pod form: the kernel runs at the rate of its mask write
-// (P*N/8 bytes, HBM) -- see DESIGN.md.
+// lane-per-pod form.  Most pods fit every node of a chunk outright (requests
+// are small against node capacity until nodes fill up): a pod whose three
+// requests are <= the chunk's smallest capacities (wave-uniform, reduced
+// once) is settled by three SCALAR compares into a 64-pod "fits everything"
+// mask, and one v_cndmask per group writes the chunk's valid-node mask for
+// all of them; only the other pods take the ballot path.  The kernel then
+// runs near the rate of its mask write (P*N/8 bytes, HBM) -- see DESIGN.md.
 #include "nas_internal.h"
 
 namespace nas {
@@ -59,13 +64,33 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
         fm = __hip_atomic_load(cp + N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         fp = __hip_atomic_load(cp + 2 * (size_t)N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // the chunk's valid nodes and its smallest capacities (padding lanes
+    // excluded: they fit nothing), wave-uniform
+    const unsigned long long valid = __builtin_amdgcn_ballot_w64(nl < nloc);
+    int mc = nl < nloc ? fc : 0x7fffffff, mm = nl < nloc ? fm : 0x7fffffff;
+    int mp = nl < nloc ? fp : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        mc = min(mc, __shfl_xor(mc, o));
+        mm = min(mm, __shfl_xor(mm, o));
+        mp = min(mp, __shfl_xor(mp, o));
+    }
+    mc = __builtin_amdgcn_readfirstlane(mc);
+    mm = __builtin_amdgcn_readfirstlane(mm);
+    mp = __builtin_amdgcn_readfirstlane(mp);
+    const unsigned vlo = (unsigned)valid, vhi = (unsigned)(valid >> 32);
     const int pend = min(p_end, pb0 + block_pods);
     for (int pb = pb0; pb < pend; pb += 64) {
         unsigned lo = 0, hi = 0;
+        unsigned long long all_fit = 0;  // pods of the group that fit every valid node
         // lane i takes pod pb + i's word: three v_cmp of the pod's (uniform)
         // requests against the lanes' capacities straight into SGPR lane
         // masks, ANDed on the scalar unit, v_writelane into lane i
         auto pod = [&](int i, int ra, int rb, int rd) {
+            if (ra <= mc && rb <= mm && rd <= mp) {  // uniform: scalar compares only
+                all_fit |= 1ull << i;
+                return;
+            }
             const unsigned long long m = __builtin_amdgcn_ballot_w64(ra <= fc) &
                                          __builtin_amdgcn_ballot_w64(rb <= fm) &
                                          __builtin_amdgcn_ballot_w64(rd <= fp);
@@ -93,6 +118,10 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
             for (int i = 0; i < 64; ++i)
                 pod(i, __builtin_amdgcn_readlane(va, i), __builtin_amdgcn_readlane(vb, i),
                     __builtin_amdgcn_readlane(vd, i));
+        }
+        if ((all_fit >> lane) & 1) {
+            lo = vlo;
+            hi = vhi;
         }
         if (pb + lane < pend) mask[(size_t)c * Pp + pb + lane] = ((unsigned long long)hi << 32) | lo;
     }

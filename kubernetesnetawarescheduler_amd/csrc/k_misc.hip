@@ -135,6 +135,8 @@ __device__ __forceinline__ T from_int(int v);
 template <>
 __device__ __forceinline__ signed char from_int<signed char>(int v) { return (signed char)v; }
 template <>
+__device__ __forceinline__ float from_int<float>(int v) { return (float)v; }
+template <>
 __device__ __forceinline__ unsigned short from_int<unsigned short>(int v) {
     // round to nearest even (exact for |v| <= 256)
     const unsigned u = __float_as_uint((float)v);
@@ -292,6 +294,14 @@ __global__ void k_plane_scatter(const int *__restrict__ pod, const int *__restri
         WA[(size_t)pod[i] * Kp + node[i]] = val[i];
 }
 
+__global__ void k_scatter_f32(const int *__restrict__ pod, const int *__restrict__ node,
+                              const float *__restrict__ val, long long n, int Kp,
+                              float *__restrict__ WA) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        WA[(size_t)pod[i] * Kp + node[i]] = val[i];
+}
+
 // Lr[m][i] = Lt[i][m], m < N, i < Mp: 64 x 64 tiles through LDS
 __global__ void k_make_lr(const signed char *__restrict__ Lt, int N, int Mp, int Kp,
                           signed char *__restrict__ Lr) {
@@ -389,6 +399,9 @@ hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int 
         k_transpose<signed char><<<grid, 256, 0, st>>>(static_cast<const signed char *>(L_dev), N,
                                                        n0, nloc, Mp, Kp,
                                                        static_cast<signed char *>(Lt));
+    else if (dtype == NAS_DT_F32)
+        k_transpose<float><<<grid, 256, 0, st>>>(static_cast<const float *>(L_dev), N, n0, nloc, Mp,
+                                                 Kp, static_cast<float *>(Lt));
     else
         k_transpose<unsigned short><<<grid, 256, 0, st>>>(
             static_cast<const unsigned short *>(L_dev), N, n0, nloc, Mp, Kp,
@@ -407,6 +420,13 @@ hipError_t launch_plane_scatter(hipStream_t st, const int32_t *pod, const int32_
                                 const signed char *val, int64_t n, int Kp, signed char *WA) {
     if (n <= 0) return hipSuccess;
     k_plane_scatter<<<grid_for(n, 256), 256, 0, st>>>(pod, node, val, (long long)n, Kp, WA);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_f32(hipStream_t st, const int32_t *pod, const int32_t *node,
+                              const float *val, int64_t n, int Kp, float *WA) {
+    if (n <= 0) return hipSuccess;
+    k_scatter_f32<<<grid_for(n, 256), 256, 0, st>>>(pod, node, val, (long long)n, Kp, WA);
     return hipGetLastError();
 }
 
@@ -448,45 +468,43 @@ hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int lo, 
     return hipGetLastError();
 }
 
-hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
-                                int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
-                                int32_t *cap, int32_t *req, void *L_full) {
+template <typename T>
+hipError_t synth_cluster_t(hipStream_t st, uint64_t seed, int N, int P, int peers, int n0, int nloc,
+                           int Mp, int Kp, int Pp, void *Lt, void *WA, int32_t *req, void *L_full) {
     hipError_t e;
     if (Lt) {
-        if (dtype == NAS_DT_I8)
-            k_synth_lt<signed char><<<grid_for((long long)Mp * Kp, 256), 256, 0, st>>>(
-                seed, N, n0, nloc, Mp, Kp, static_cast<signed char *>(Lt));
-        else
-            k_synth_lt<unsigned short><<<grid_for((long long)Mp * Kp, 256), 256, 0, st>>>(
-                seed, N, n0, nloc, Mp, Kp, static_cast<unsigned short *>(Lt));
+        k_synth_lt<T><<<grid_for((long long)Mp * Kp, 256), 256, 0, st>>>(seed, N, n0, nloc, Mp, Kp,
+                                                                         static_cast<T *>(Lt));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (L_full) {
-        if (dtype == NAS_DT_I8)
-            k_synth_lfull<signed char><<<grid_for((long long)N * N, 256), 256, 0, st>>>(
-                seed, N, static_cast<signed char *>(L_full));
-        else
-            k_synth_lfull<unsigned short><<<grid_for((long long)N * N, 256), 256, 0, st>>>(
-                seed, N, static_cast<unsigned short *>(L_full));
+        k_synth_lfull<T><<<grid_for((long long)N * N, 256), 256, 0, st>>>(seed, N,
+                                                                          static_cast<T *>(L_full));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (WA) {
         const long long tot = (long long)Pp * Kp;
-        if (dtype == NAS_DT_I8)
-            k_synth_bg<signed char><<<grid_for(tot, 256), 256, 0, st>>>(
-                seed, N, P, Kp, tot, static_cast<signed char *>(WA));
-        else
-            k_synth_bg<unsigned short><<<grid_for(tot, 256), 256, 0, st>>>(
-                seed, N, P, Kp, tot, static_cast<unsigned short *>(WA));
+        k_synth_bg<T><<<grid_for(tot, 256), 256, 0, st>>>(seed, N, P, Kp, tot, static_cast<T *>(WA));
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (dtype == NAS_DT_I8)
-            k_synth_pods<signed char><<<(Pp + 255) / 256, 256, 0, st>>>(
-                seed, N, P, peers, Kp, Pp, static_cast<signed char *>(WA), req);
-        else
-            k_synth_pods<unsigned short><<<(Pp + 255) / 256, 256, 0, st>>>(
-                seed, N, P, peers, Kp, Pp, static_cast<unsigned short *>(WA), req);
+        k_synth_pods<T><<<(Pp + 255) / 256, 256, 0, st>>>(seed, N, P, peers, Kp, Pp,
+                                                           static_cast<T *>(WA), req);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    return hipSuccess;
+}
+
+hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
+                                int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
+                                int32_t *cap, int32_t *req, void *L_full) {
+    hipError_t e = dtype == NAS_DT_I8
+                       ? synth_cluster_t<signed char>(st, seed, N, P, peers, n0, nloc, Mp, Kp, Pp,
+                                                      Lt, WA, req, L_full)
+                   : dtype == NAS_DT_F32
+                       ? synth_cluster_t<float>(st, seed, N, P, peers, n0, nloc, Mp, Kp, Pp, Lt, WA,
+                                                req, L_full)
+                       : synth_cluster_t<unsigned short>(st, seed, N, P, peers, n0, nloc, Mp, Kp,
+                                                         Pp, Lt, WA, req, L_full);
+    if (e != hipSuccess) return e;
     if (cap) {
         k_synth_cap<<<(N + 255) / 256, 256, 0, st>>>(seed, N, cap);
         if ((e = hipGetLastError()) != hipSuccess) return e;

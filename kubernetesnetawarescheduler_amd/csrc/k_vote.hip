@@ -191,14 +191,17 @@ k_vote(const double *__restrict__ cpu, const double *__restrict__ mem,
        const long long *__restrict__ tx, const long long *__restrict__ disk, int n, long long ns,
        const int *__restrict__ order1, const int *__restrict__ pos1,
        const int *__restrict__ pos2, long long ord_ns, int n_orders,
-       int *__restrict__ best_out, int *__restrict__ win_out) {
-    const int s = blockIdx.x;
-    const int o = n_orders == 1 ? 0 : s;
+       int *__restrict__ best_out, int *__restrict__ win_out, const int *__restrict__ pod_snap) {
+    // block b: one snapshot (pod_snap null), or one pod scoring snapshot
+    // pod_snap[b] with its own order set b (nas_upload_pod_orders)
+    const int b = blockIdx.x;
+    const int s = pod_snap ? pod_snap[b] : b;
+    const int o = n_orders == 1 ? 0 : b;
     const VoteAcc a = reduce_snapshot<false>(cpu, mem, bw, rx, tx, disk, (size_t)s * ns, 0, n,
                                              pos1 + (size_t)o * ord_ns);
     if (threadIdx.x != 0) return;
-    vote_decide(a, n, order1 + (size_t)o * ord_ns, pos2 + (size_t)o * (ord_ns + 2), best_out + s,
-                win_out ? win_out + (size_t)s * 6 : nullptr);
+    vote_decide(a, n, order1 + (size_t)o * ord_ns, pos2 + (size_t)o * (ord_ns + 2), best_out + b,
+                win_out ? win_out + (size_t)b * 6 : nullptr);
 }
 
 // Node-shard partial: the six extrema of nodes [lo, lo + nl) -> part[s]
@@ -272,7 +275,18 @@ hipError_t launch_vote(hipStream_t st, const nas_ctx *c, int S) {
         c->snap[0].as<double>(), c->snap[1].as<double>(), c->snap[2].as<double>(),
         c->snap[3].as<long long>(), c->snap[4].as<long long>(), c->snap[5].as<long long>(),
         c->snap_n, c->snap_ns, c->order1.as<int>(), c->pos1.as<int>(), c->pos2.as<int>(),
-        c->ord_ns, c->n_orders, c->snap_best.as<int>(), c->snap_win.as<int>());
+        c->ord_ns, c->n_orders, c->snap_best.as<int>(), c->snap_win.as<int>(), nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_vote_pods(hipStream_t st, const nas_ctx *c, const int32_t *pod_snap, int P,
+                            int32_t *best, int32_t *win) {
+    if (P <= 0) return hipSuccess;
+    k_vote<<<P, VOTE_THREADS, 0, st>>>(
+        c->snap[0].as<double>(), c->snap[1].as<double>(), c->snap[2].as<double>(),
+        c->snap[3].as<long long>(), c->snap[4].as<long long>(), c->snap[5].as<long long>(),
+        c->snap_n, c->snap_ns, c->order1.as<int>(), c->pos1.as<int>(), c->pos2.as<int>(),
+        c->ord_ns, c->n_orders, best, win, pod_snap);
     return hipGetLastError();
 }
 

@@ -94,9 +94,14 @@ int bind(nas_ctx *ctx) {
     return NAS_OK;
 }
 
-size_t esz(int dtype) { return dtype == NAS_DT_I8 ? 1 : 2; }
+size_t esz(int dtype) { return dtype == NAS_DT_I8 ? 1 : dtype == NAS_DT_F32 ? 4 : 2; }
 
-int64_t kpad(int n, int dtype) { return nas::round_up(n, dtype == NAS_DT_I8 ? 128 : 64); }
+// contraction length padded to whole 128-byte K-steps of the cost kernel
+int64_t kpad(int n, int dtype) { return nas::round_up(n, 128 / (int)esz(dtype)); }
+
+bool valid_dtype(int dtype) {
+    return dtype == NAS_DT_I8 || dtype == NAS_DT_BF16 || dtype == NAS_DT_F32;
+}
 
 // event pool for per-stage device timing on the context stream
 struct Timer {
@@ -147,7 +152,8 @@ int validate_perm(const int32_t *o, int n, std::vector<int32_t> &pos) {
     return 0;
 }
 
-int upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, int32_t n_orders) {
+int upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, int32_t n_orders,
+                  bool per_pod = false) {
     const int n = ctx->snap_n;
     if (n <= 0) return nas::fail(ctx, NAS_ERR_STATE, "upload a snapshot before its orders");
     if (!order1 || !order2 || n_orders <= 0) return nas::fail(ctx, NAS_ERR_ARG, "orders");
@@ -177,6 +183,7 @@ int upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, in
     HIPCK(hipMemcpyAsync(ctx->pos2.p, p2.data(), p2.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));  // host vectors die here
     ctx->n_orders = n_orders;
+    ctx->orders_per_pod = per_pod;
     ctx->ord_ns = ns;
     return NAS_OK;
 }
@@ -899,14 +906,23 @@ int upload_snapshot_slice(nas_ctx *ctx, const double *cpu, const double *mem, co
 }
 
 // nas_score_reference's argument checks and order upload, shared by the
-// node-shard entries.
-int prepare_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2) {
+// node-shard entries.  Per-snapshot sets must cover the `need` snapshots the
+// call votes on; per-pod sets (nas_upload_pod_orders) are checked by the caller.
+int prepare_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, int need,
+                   bool pods_ok = false) {
     if (ctx->snap_s <= 0) return nas::fail(ctx, NAS_ERR_STATE, "no snapshot uploaded");
     if ((order1 == nullptr) != (order2 == nullptr))
         return nas::fail(ctx, NAS_ERR_ARG, "order1 and order2 must both be given or both NULL");
     if (order1) OK(upload_orders(ctx, order1, order2, 1));
-    if (ctx->n_orders != 1 && ctx->n_orders != ctx->snap_s)
-        return nas::fail(ctx, NAS_ERR_STATE, "orders: need 1 set or one per snapshot");
+    if (ctx->n_orders <= 0) return nas::fail(ctx, NAS_ERR_STATE, "no orders uploaded");
+    if (ctx->orders_per_pod) {
+        if (!pods_ok)
+            return nas::fail(ctx, NAS_ERR_STATE,
+                             "per-pod order sets serve nas_score_reference on an unsharded snapshot only");
+        return NAS_OK;
+    }
+    if (ctx->n_orders != 1 && ctx->n_orders < need)
+        return nas::fail(ctx, NAS_ERR_STATE, "orders: need 1 set or one per snapshot voted on");
     return NAS_OK;
 }
 }  // namespace
@@ -931,7 +947,7 @@ int nas_upload_snapshot_shard(nas_ctx *ctx, const double *cpu, const double *mem
 int nas_vote_partials(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, int32_t S,
                       nas_vote_partial *out) {
     OK(bind(ctx));
-    OK(prepare_orders(ctx, order1, order2));
+    OK(prepare_orders(ctx, order1, order2, S));
     if (S < 0 || S > ctx->snap_s || (S > 0 && !out))
         return nas::fail(ctx, NAS_ERR_ARG, "nas_vote_partials: S / out");
     if (S == 0) return NAS_OK;
@@ -955,7 +971,7 @@ int nas_vote_partials(nas_ctx *ctx, const int32_t *order1, const int32_t *order2
 int nas_vote_merge(nas_ctx *ctx, const nas_vote_partial *parts, int32_t n_parts, int32_t S,
                    int32_t *best_out, int32_t *winners_out) {
     OK(bind(ctx));
-    OK(prepare_orders(ctx, nullptr, nullptr));
+    OK(prepare_orders(ctx, nullptr, nullptr, 1));
     if (n_parts < 1 || S < 0 || (S > 0 && (!parts || !best_out)))
         return nas::fail(ctx, NAS_ERR_ARG, "nas_vote_merge: parts / n_parts / S / best_out");
     if (ctx->n_orders != 1 && S > ctx->n_orders)
@@ -995,13 +1011,23 @@ int nas_upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2
     return upload_orders(ctx, order1, order2, n_orders);
 }
 
+int nas_upload_pod_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
+                          int32_t n_pods) {
+    OK(bind(ctx));
+    return upload_orders(ctx, order1, order2, n_pods, true);
+}
+
 int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
                         const int32_t *pod_snapshot, int32_t P, int32_t *best_out,
                         int32_t *winners_out) {
     OK(bind(ctx));
     if (ctx->snap_s <= 0) return nas::fail(ctx, NAS_ERR_STATE, "no snapshot uploaded");
     if (P < 0 || (P > 0 && !best_out)) return nas::fail(ctx, NAS_ERR_ARG, "P / best_out");
-    OK(prepare_orders(ctx, order1, order2));
+    const bool per_pod = ctx->orders_per_pod && !order1;
+    OK(prepare_orders(ctx, order1, order2, pod_snapshot ? ctx->snap_s : P, !ctx->snap_sharded));
+    if (per_pod && ctx->n_orders != P)
+        return nas::fail(ctx, NAS_ERR_ARG, "per-pod order sets: P must equal the uploaded set count (" +
+                                               std::to_string(ctx->n_orders) + ")");
     if (ctx->snap_sharded && !exchanging(ctx))
         return nas::fail(ctx, NAS_ERR_STATE,
                          "node-sharded snapshot: nas_score_reference needs nas_comm_init "
@@ -1020,7 +1046,26 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     hipEvent_t a = tm.mark(), b = nullptr;
     const int Sused = pod_snapshot ? S : P;
-    if (ctx->snap_sharded) {
+    const int32_t *best_d = ctx->snap_best.as<int32_t>();
+    const int32_t *win_d = ctx->snap_win.as<int32_t>();
+    if (per_pod) {
+        // one block per pod: its snapshot, its own order set; no per-pod
+        // snapshot copies and no gather
+        OK(nas::ensure(ctx, ctx->best, (size_t)P * 4));
+        OK(nas::ensure(ctx, ctx->winners, (size_t)P * 24));
+        const int32_t *ps = nullptr;
+        if (pod_snapshot) {
+            OK(nas::ensure(ctx, ctx->pod_snap, (size_t)P * 4));
+            HIPCK(hipMemcpyAsync(ctx->pod_snap.p, pod_snapshot, (size_t)P * 4, hipMemcpyHostToDevice,
+                                 ctx->stream));
+            ps = ctx->pod_snap.as<int32_t>();
+        }
+        HIPCK(nas::launch_vote_pods(ctx->stream, ctx, ps, P, ctx->best.as<int32_t>(),
+                                    ctx->winners.as<int32_t>()));
+        b = tm.mark();
+        best_d = ctx->best.as<int32_t>();
+        win_d = ctx->winners.as<int32_t>();
+    } else if (ctx->snap_sharded) {
         // node shards: partial records of this rank's slice, all-gathered
         // over RCCL, merged in rank order (every rank gets the full result)
         const size_t rb = (size_t)Sused * sizeof(nas_vote_partial);
@@ -1040,9 +1085,7 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
         HIPCK(nas::launch_vote(ctx->stream, ctx, Sused));
         b = tm.mark();
     }
-    const int32_t *best_d = ctx->snap_best.as<int32_t>();
-    const int32_t *win_d = ctx->snap_win.as<int32_t>();
-    if (pod_snapshot) {
+    if (pod_snapshot && !per_pod) {
         OK(nas::ensure(ctx, ctx->pod_snap, (size_t)P * 4));
         OK(nas::ensure(ctx, ctx->best, (size_t)P * 4));
         OK(nas::ensure(ctx, ctx->winners, (size_t)P * 24));
@@ -1084,7 +1127,7 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
 // ----------------------------------------------------------------- extended
 int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
     OK(bind(ctx));
-    if (!L || n <= 0 || (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
+    if (!L || n <= 0 || !valid_dtype(dtype))
         return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_latency: L / n / dtype");
     set_geometry(ctx, n, dtype);
     if (dtype == NAS_DT_I8) {  // max |L| over the whole matrix (the same on every rank)
@@ -1196,7 +1239,7 @@ int nas_upload_pods(nas_ctx *ctx, const int32_t *rc, const int32_t *rm, const in
 
 // dtype here is the COMPUTE dtype (NAS_DT_I8 for int8 / int32 traffic)
 static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
-    if (P <= 0 || n <= 0 || (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
+    if (P <= 0 || n <= 0 || !valid_dtype(dtype))
         return nas::fail(ctx, NAS_ERR_ARG, "traffic: P / n / dtype");
     if (!ctx->have_L || ctx->L_n != n || ctx->L_dtype != dtype) {
         set_geometry(ctx, n, dtype);
@@ -1271,13 +1314,61 @@ int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *
     OK(bind(ctx));
     if (!row_ptr || nnz < 0 || (nnz > 0 && (!peer_node || !weight)))
         return nas::fail(ctx, NAS_ERR_ARG, "csr arrays");
-    if (dtype != NAS_DT_I8 && dtype != NAS_DT_I32 && dtype != NAS_DT_BF16)
+    if (dtype != NAS_DT_I8 && dtype != NAS_DT_I32 && dtype != NAS_DT_BF16 && dtype != NAS_DT_F32)
         return nas::fail(ctx, NAS_ERR_ARG, "csr weight dtype");
     if (ctx->B > 1) return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "CSR traffic with a cluster batch");
     if (P <= 0 || row_ptr[0] != 0 || row_ptr[P] != nnz)
         return nas::fail(ctx, NAS_ERR_ARG, "row_ptr bounds");
     for (int p = 0; p < P; ++p)
         if (row_ptr[p + 1] < row_ptr[p]) return nas::fail(ctx, NAS_ERR_ARG, "row_ptr not monotone");
+    if (dtype == NAS_DT_F32) {
+        // fp32 traffic: per-node sums in fp64 on the host, rounded to fp32
+        // once, scattered into the dense rows on the device
+        OK(traffic_common(ctx, NAS_DT_F32, P, n));
+        std::vector<int32_t> tp, tn;
+        std::vector<float> tv;
+        std::vector<std::pair<int32_t, double>> agg;
+        const auto *wf = static_cast<const float *>(weight);
+        for (int p = 0; p < P; ++p) {
+            agg.clear();
+            for (int64_t x = row_ptr[p]; x < row_ptr[p + 1]; ++x)
+                if (peer_node[x] >= 0 && peer_node[x] < n) agg.push_back({peer_node[x], (double)wf[x]});
+            std::sort(agg.begin(), agg.end(),
+                      [](const auto &a, const auto &b) { return a.first < b.first; });
+            for (size_t i = 0; i < agg.size();) {
+                const int32_t m = agg[i].first;
+                double v = 0;
+                for (; i < agg.size() && agg[i].first == m; ++i) v += agg[i].second;
+                tp.push_back(p);
+                tn.push_back(m);
+                tv.push_back((float)v);
+            }
+        }
+        DevBuf dp, dn, dv;
+        int rc = nas::ensure(ctx, dp, tp.size() * 4 + 4);
+        if (rc == NAS_OK) rc = nas::ensure(ctx, dn, tn.size() * 4 + 4);
+        if (rc == NAS_OK) rc = nas::ensure(ctx, dv, tv.size() * 4 + 4);
+        hipError_t he = hipSuccess;
+        if (rc == NAS_OK && !tp.empty()) {
+            he = hipMemcpyAsync(dp.p, tp.data(), tp.size() * 4, hipMemcpyHostToDevice, ctx->stream);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(dn.p, tn.data(), tn.size() * 4, hipMemcpyHostToDevice, ctx->stream);
+            if (he == hipSuccess)
+                he = hipMemcpyAsync(dv.p, tv.data(), tv.size() * 4, hipMemcpyHostToDevice, ctx->stream);
+            if (he == hipSuccess)
+                he = nas::launch_scatter_f32(ctx->stream, dp.as<int32_t>(), dn.as<int32_t>(),
+                                             dv.as<float>(), (int64_t)tp.size(), ctx->Kp,
+                                             ctx->WA.as<float>());
+        }
+        (void)hipStreamSynchronize(ctx->stream);
+        for (DevBuf *b : {&dp, &dn, &dv})
+            if (b->p) (void)hipFree(b->p);
+        if (rc != NAS_OK) return rc;
+        if (he != hipSuccess) return nas::hip_fail(ctx, he, "csr f32 scatter");
+        ctx->have_wa = true;
+        ctx->synth_valid = false;
+        return NAS_OK;
+    }
     if (dtype != NAS_DT_BF16) {
         // exact integer aggregation on the host (int64 sums, then int32 range):
         // the plane entries are scattered on the device, the rest is overflow
@@ -1859,8 +1950,7 @@ int nas_set_batch(nas_ctx *ctx, int32_t n_clusters) {
 
 static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_t P,
                  int32_t dtype, int32_t peers) {
-    if (n_nodes <= 0 || P <= 0 || peers < 1 || peers > 16 || B < 1 ||
-        (dtype != NAS_DT_I8 && dtype != NAS_DT_BF16))
+    if (n_nodes <= 0 || P <= 0 || peers < 1 || peers > 16 || B < 1 || !valid_dtype(dtype))
         return nas::fail(ctx, NAS_ERR_ARG, "nas_synth_cluster arguments");
     if (B > 1 && ctx->world > 1)
         return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");

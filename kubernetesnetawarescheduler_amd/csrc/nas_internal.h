@@ -76,6 +76,7 @@ struct nas_ctx {
     int64_t snap_ns = 0;              // padded row stride of the slice (even)
     nas::DevBuf snap[6];              // cpu, mem, bw (f64) ; rx, tx, disk (i64)  [S][ns]
     int32_t n_orders = 0;
+    bool orders_per_pod = false;      // nas_upload_pod_orders: set p belongs to pod p
     int64_t ord_ns = 0;               // row stride of order arrays
     nas::DevBuf order1, pos1;         // [n_orders][ord_ns]
     nas::DevBuf order2, pos2;         // [n_orders][ord_ns + 2]  (n+1 keys)
@@ -172,6 +173,10 @@ int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes);
 
 // kernel launchers (k_*.hip); all enqueue on `stream` and return hipError_t
 hipError_t launch_vote(hipStream_t st, const nas_ctx *c, int n_snapshots_used);
+// per-pod order sets (nas_upload_pod_orders): pod p scores snapshot
+// pod_snap[p] (device array) with order set p -> best[p], win[p][6]
+hipError_t launch_vote_pods(hipStream_t st, const nas_ctx *c, const int32_t *pod_snap, int P,
+                            int32_t *best, int32_t *win);
 // node-shard form: partial records of the context's slice -> part[S]
 hipError_t launch_vote_partial(hipStream_t st, const nas_ctx *c, int S, nas_vote_partial *part);
 // merge parts[n_parts][S] -> best[S], win[S][6] with the context's orders
@@ -243,6 +248,9 @@ hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int 
 // bf16 CSR traffic -> dense WA rows (fp32 sums, rounded once)
 hipError_t launch_csr_aggregate_bf16(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
                                      const uint16_t *w, int P, int N, int Kp, uint16_t *WA);
+// fp32 rows WA[p][m] = v for host-aggregated (pod, node, value) triples
+hipError_t launch_scatter_f32(hipStream_t st, const int32_t *pod, const int32_t *node,
+                              const float *val, int64_t n, int Kp, float *WA);
 // int8 plane entries WA[p][m] = v for host-aggregated (pod, node, value) triples
 hipError_t launch_plane_scatter(hipStream_t st, const int32_t *pod, const int32_t *node,
                                 const signed char *val, int64_t n, int Kp, signed char *WA);

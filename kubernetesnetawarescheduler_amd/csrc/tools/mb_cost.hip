@@ -3,6 +3,7 @@
 // events over back-to-back launches on random operands, interleaved.
 #define NAS_DIAG_VARIANTS
 #include "../k_cost.hip"
+#include "k_cost_experiments.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -18,7 +19,7 @@ int main(int argc, char **argv) {
     const int P = argc > 2 ? atoi(argv[2]) : 100000;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
     const char *vsel = argc > 4 ? argv[4] : "abcdefgh";  // variants to run (a..)
-    const int Mp = (int)round_up(N, 256), Kp = (int)round_up(N, 128), Pp = (int)round_up(P, 256);
+    const int Mp = (int)round_up(N, 256), Kp = (int)round_up(N, 256), Pp = (int)round_up(P, 256);
     void *Lt, *WA, *mask, *partial, *pbound;
     CK(hipMalloc(&Lt, (size_t)Mp * Kp));
     CK(hipMalloc(&WA, (size_t)Pp * Kp));
@@ -31,7 +32,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(Lt, h.data(), (size_t)Mp * Kp, hipMemcpyHostToDevice));
     CK(hipMemset(mask, 0xff, (size_t)(Mp / 64) * Pp * 8));
     // variants: name, kernel
-    struct V { const char *name; const void *fn; int lds; };
+    struct V { const char *name; const void *fn; int lds; int threads = THREADS; };
 #define KV(E, S, PP, G) (const void *)&k_cost_topk<NAS_DT_I8, E, S, PP, G>, lds_bytes<PP>()
     const V vars[] = {{"top4/jit", KV(0, 0, 0, 4)},   {"noepi/jit", KV(1, 0, 0, 4)},
                       {"top4/spread", KV(0, 5, 0, 4)}, {"noepi/spread", KV(1, 5, 0, 4)},
@@ -49,7 +50,11 @@ int main(int argc, char **argv) {
                       {"v2/top4/st4", KV2(0, 4, 4)}, {"v2/noepi/st4", KV2(1, 4, 4)},
                       {"v2/l2hot", KV2(3, 4, 4)}, {"v2/ldsonly", KV2(4, 4, 4)},
                       {"v2/top4/st3", KV2(0, 3, 4)}, {"v2/top4/g8", KV2(0, 4, 8)},
-                      {"v2/noepi/st3", KV2(1, 3, 4)}};
+                      {"v2/noepi/st3", KV2(1, 3, 4)},
+#define KV3(E, S, G) (const void *)&k_cost_topk3<NAS_DT_I8, E, S, G>, (S) * TILE_BYTES
+                      {"v3/top4", KV3(0, 4, 4)}, {"v3/noepi", KV3(1, 4, 4)},
+                      {"v3/l2hot", KV3(3, 4, 4)}, {"v3/ldsonly", KV3(4, 4, 4)},
+                      {"v3/top4/g8", KV3(0, 4, 8)}};
     const int nv = sizeof(vars) / sizeof(vars[0]);
     for (int v = 0; v < nv; ++v)
         CK(hipFuncSetAttribute(vars[v].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[v].lds));
@@ -70,7 +75,8 @@ int main(int argc, char **argv) {
             void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero,
                             (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf};
             CK(hipEventRecord(a));
-            CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(THREADS), args, vars[v].lds, 0));
+            const int thr = strncmp(vars[v].name, "v3", 2) ? THREADS : THREADS3;
+            CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(thr), args, vars[v].lds, 0));
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms;

@@ -129,6 +129,12 @@ class Engine:
         n_orders = 1 if o1.ndim == 1 else o1.shape[0]
         self._ck(self._L.nas_upload_orders(self._h, ptr(o1), ptr(o2), n_orders))
 
+    def upload_pod_orders(self, order1, order2):
+        """One order set per pod of the next score_reference (include/nas.h)."""
+        o1 = np.atleast_2d(as_c(order1, np.int32))
+        o2 = np.atleast_2d(as_c(order2, np.int32))
+        self._ck(self._L.nas_upload_pod_orders(self._h, ptr(o1), ptr(o2), o1.shape[0]))
+
     def score_reference(self, P=None, order1=None, order2=None, pod_snapshot=None, winners=True):
         ps = None if pod_snapshot is None else as_c(pod_snapshot, np.int32)
         if P is None:
@@ -201,11 +207,11 @@ class Engine:
 
     @staticmethod
     def _dt(dtype):
-        return {"i8": _lib.NAS_DT_I8, "bf16": _lib.NAS_DT_BF16}[dtype]
+        return {"i8": _lib.NAS_DT_I8, "bf16": _lib.NAS_DT_BF16, "f32": _lib.NAS_DT_F32}[dtype]
 
     @staticmethod
     def _np(dtype):
-        return np.int8 if dtype == "i8" else np.uint16
+        return {"i8": np.int8, "bf16": np.uint16, "f32": np.float32}[dtype]
 
     # A batch (set_batch / synth_batch) passes every extended-mode array with a
     # leading cluster axis: L (B, n, n), free (B, n, 3), req (B, P, 3), WA (B, P, n).
@@ -266,14 +272,14 @@ class Engine:
 
     def upload_traffic(self, WA, dtype):
         """dtype "i8": integer traffic (int8 arrays as int8, wider ones as exact
-        int32) against int8 latency; "bf16": bf16 bits."""
+        int32) against int8 latency; "bf16": bf16 bits; "f32": float32."""
         if dtype in ("i8", "i32"):
             WA, dt = self._int_traffic(WA)
         else:
             WA, dt = as_c(WA, self._np(dtype)), self._dt(dtype)
         P, n = WA.shape[-2:]
         self._ck(self._L.nas_upload_traffic_dense(self._h, ptr(WA), dt, P, n))
-        self.n_pods, self.n_nodes, self.dtype = P, n, "bf16" if dtype == "bf16" else "i8"
+        self.n_pods, self.n_nodes, self.dtype = P, n, "i8" if dtype in ("i8", "i32") else dtype
 
     def upload_traffic_csr(self, row_ptr, peer_node, weight, dtype, n):
         rp = as_c(row_ptr, np.int32)
@@ -285,7 +291,7 @@ class Engine:
         P = rp.shape[0] - 1
         self._ck(self._L.nas_upload_traffic_csr(self._h, ptr(rp), ptr(pn), ptr(w), dt,
                                                 P, n, pn.shape[0]))
-        self.n_pods, self.n_nodes, self.dtype = P, n, "bf16" if dtype == "bf16" else "i8"
+        self.n_pods, self.n_nodes, self.dtype = P, n, "i8" if dtype in ("i8", "i32") else dtype
 
     def filter(self):
         chunks = (self.n_nodes + 63) // 64

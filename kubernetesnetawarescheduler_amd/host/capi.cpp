@@ -192,6 +192,21 @@ int nas_host_latency_matrix(int32_t n, const char *const *reports, const size_t 
     return NAS_OK;
 }
 
+float nas_host_latency_us_from_bps(double bps) { return latency_us_from_bps(bps); }
+
+int nas_host_latency_matrix_us(int32_t n, const char *const *reports, const size_t *report_len,
+                               float *L_out) {
+    if (n <= 0 || !reports || !report_len || !L_out) return NAS_ERR_ARG;
+    const std::vector<float> L = latency_matrix_us(n, [&](int i, int j, std::string &bytes) {
+        const size_t k = (size_t)i * n + j;
+        if (!reports[k]) return false;
+        bytes.assign(reports[k], report_len[k]);
+        return true;
+    });
+    std::memcpy(L_out, L.data(), L.size() * sizeof(float));
+    return NAS_OK;
+}
+
 int nas_host_create(nas_host_sched **out, nas_ctx *ctx, const nas_host_io *io) {
     if (!out || !ctx || !io) return NAS_ERR_ARG;
     auto *s = new (std::nothrow) nas_host_sched;
@@ -230,6 +245,17 @@ int nas_host_set_latency(nas_host_sched *s, const char *const *names, const int8
         std::vector<std::string> nm;
         for (int i = 0; i < n; ++i) nm.push_back(names[i] ? names[i] : "");
         s->s->set_latency(nm, std::vector<int8_t>(L, L + (size_t)n * n));
+        return NAS_OK;
+    })
+}
+
+int nas_host_set_latency_f32(nas_host_sched *s, const char *const *names, const float *L,
+                             int32_t n) {
+    if (!s || !names || !L || n <= 0) return NAS_ERR_ARG;
+    GUARD(s, {
+        std::vector<std::string> nm;
+        for (int i = 0; i < n; ++i) nm.push_back(names[i] ? names[i] : "");
+        s->s->set_latency_f32(nm, std::vector<float>(L, L + (size_t)n * n));
         return NAS_OK;
     })
 }

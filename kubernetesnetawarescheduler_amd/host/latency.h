@@ -27,4 +27,13 @@ int8_t latency_from_bps(double bps);
 std::vector<int8_t> latency_matrix(int n,
                                    const std::function<bool(int, int, std::string &)> &report);
 
+// The unquantised form for the fp32 path (NAS_DT_F32): microseconds to move
+// 1 MB, 8e12 / bps, as float; an unusable pair (no report, bps <= 0 or NaN)
+// costs kUnusableUs, +Inf bps costs 0.  Symmetric (the slower direction),
+// 0 on the diagonal.
+constexpr float kUnusableUs = 1e7f;  // 10 s per MB: never preferred, never Inf/NaN
+float latency_us_from_bps(double bps);
+std::vector<float> latency_matrix_us(int n,
+                                     const std::function<bool(int, int, std::string &)> &report);
+
 }  // namespace nas_host

@@ -71,25 +71,28 @@ void CustomScheduler::scrape() {
 int CustomScheduler::vote(int P, const std::vector<int32_t> &o1, const std::vector<int32_t> &o2,
                           std::vector<int32_t> &best, std::vector<int32_t> &winners) {
     const int n = (int)metrics_.size();
-    // one snapshot copy per pod so that every pod carries its own map orders
-    std::vector<double> cpu, mem, bw;
-    std::vector<int64_t> rx, tx, disk;
-    for (int p = 0; p < P; ++p)
-        for (const NodeMetrics &m : metrics_) {
-            cpu.push_back(m.cpu_frequency_hertz);
-            mem.push_back(m.occupied_memory_percentage);
-            rx.push_back(m.network_packets_received);
-            tx.push_back(m.network_packets_sent);
-            bw.push_back(m.network_bandwidth);
-            disk.push_back(m.disk_io_now);
-        }
+    // ONE snapshot (the scrape every pod of the batch sees); each pod walks
+    // its own map orders (nas_upload_pod_orders), pod p -> snapshot 0
+    std::vector<double> cpu(n), mem(n), bw(n);
+    std::vector<int64_t> rx(n), tx(n), disk(n);
+    for (int i = 0; i < n; ++i) {
+        const NodeMetrics &m = metrics_[i];
+        cpu[i] = m.cpu_frequency_hertz;
+        mem[i] = m.occupied_memory_percentage;
+        rx[i] = m.network_packets_received;
+        tx[i] = m.network_packets_sent;
+        bw[i] = m.network_bandwidth;
+        disk[i] = m.disk_io_now;
+    }
     check(ctx_, nas_upload_snapshot(ctx_, cpu.data(), mem.data(), rx.data(), tx.data(), bw.data(),
-                                    disk.data(), n, P),
+                                    disk.data(), n, 1),
           "nas_upload_snapshot");
-    check(ctx_, nas_upload_orders(ctx_, o1.data(), o2.data(), P), "nas_upload_orders");
+    check(ctx_, nas_upload_pod_orders(ctx_, o1.data(), o2.data(), P), "nas_upload_pod_orders");
+    pod_snap_.assign(P, 0);
     best.assign(P, 0);
     winners.assign((size_t)P * 6, 0);
-    check(ctx_, nas_score_reference(ctx_, nullptr, nullptr, nullptr, P, best.data(), winners.data()),
+    check(ctx_, nas_score_reference(ctx_, nullptr, nullptr, pod_snap_.data(), P, best.data(),
+                                    winners.data()),
           "nas_score_reference");
     return n;
 }
@@ -186,10 +189,18 @@ void CustomScheduler::set_latency(const std::vector<std::string> &names, const s
     if (L.size() != names.size() * names.size()) throw std::invalid_argument("latency matrix size");
     lat_names_ = names;
     lat_ = L;
+    lat_f32_ = false;
 }
 
-std::vector<std::pair<Pod, Outcome>> CustomScheduler::place_pending(int dtype) {
-    if (dtype != NAS_DT_I8) throw std::invalid_argument("the host mirror places with int8 costs");
+void CustomScheduler::set_latency_f32(const std::vector<std::string> &names,
+                                      const std::vector<float> &L) {
+    if (L.size() != names.size() * names.size()) throw std::invalid_argument("latency matrix size");
+    lat_names_ = names;
+    lat_f_ = L;
+    lat_f32_ = true;
+}
+
+std::vector<std::pair<Pod, Outcome>> CustomScheduler::place_pending() {
     std::vector<std::pair<Pod, Outcome>> out;
     std::vector<Pod> pods(queue_.begin(), queue_.end());
     queue_.clear();
@@ -205,14 +216,17 @@ std::vector<std::pair<Pod, Outcome>> CustomScheduler::place_pending(int dtype) {
     for (size_t i = 0; i < lat_names_.size(); ++i) lat_idx[lat_names_[i]] = (int)i;
     for (int i = 0; i < n; ++i) node_idx[nodes[i]] = i;
     // L over the listed nodes (every listed node must have been measured)
-    std::vector<int8_t> L((size_t)n * n);
+    std::vector<int8_t> L(lat_f32_ ? 0 : (size_t)n * n);
+    std::vector<float> Lf(lat_f32_ ? (size_t)n * n : 0);
     for (int a = 0; a < n; ++a)
         for (int b = 0; b < n; ++b) {
             auto ia = lat_idx.find(nodes[a]), ib = lat_idx.find(nodes[b]);
             if (ia == lat_idx.end() || ib == lat_idx.end())
                 throw std::runtime_error("no latency measured for node " +
                                          (ia == lat_idx.end() ? nodes[a] : nodes[b]));
-            L[(size_t)a * n + b] = lat_[(size_t)ia->second * lat_names_.size() + ib->second];
+            const size_t src = (size_t)ia->second * lat_names_.size() + ib->second;
+            if (lat_f32_) Lf[(size_t)a * n + b] = lat_f_[src];
+            else L[(size_t)a * n + b] = lat_[src];
         }
     std::vector<int32_t> cc(n), cm(n), cp(n);
     for (int i = 0; i < n; ++i)
@@ -220,6 +234,7 @@ std::vector<std::pair<Pod, Outcome>> CustomScheduler::place_pending(int dtype) {
             throw std::runtime_error("no capacity for node " + nodes[i]);
     std::vector<int32_t> rc(P), rm(P), rp(P, 1), row_ptr(P + 1, 0), peer_node;
     std::vector<int32_t> weight;  // exact: aggregated per node in int64 by the engine
+    std::vector<float> weight_f;  // fp32 path: aggregated in fp64, rounded once
     for (int p = 0; p < P; ++p) {
         rc[p] = pods[p].cpu_milli;
         rm[p] = pods[p].mem_kib;
@@ -228,14 +243,18 @@ std::vector<std::pair<Pod, Outcome>> CustomScheduler::place_pending(int dtype) {
             auto it = node_idx.find(where);
             peer_node.push_back(it == node_idx.end() ? -1 : it->second);  // unbound: skipped
             weight.push_back(q.weight);
+            weight_f.push_back((float)q.weight);
         }
         row_ptr[p + 1] = (int32_t)peer_node.size();
     }
-    check(ctx_, nas_upload_latency(ctx_, L.data(), NAS_DT_I8, n), "nas_upload_latency");
+    if (lat_f32_) check(ctx_, nas_upload_latency(ctx_, Lf.data(), NAS_DT_F32, n), "nas_upload_latency");
+    else check(ctx_, nas_upload_latency(ctx_, L.data(), NAS_DT_I8, n), "nas_upload_latency");
     check(ctx_, nas_upload_capacity(ctx_, cc.data(), cm.data(), cp.data(), n), "nas_upload_capacity");
     check(ctx_, nas_upload_pods(ctx_, rc.data(), rm.data(), rp.data(), P), "nas_upload_pods");
-    check(ctx_, nas_upload_traffic_csr(ctx_, row_ptr.data(), peer_node.data(), weight.data(), NAS_DT_I32,
-                                       P, n, (int64_t)peer_node.size()),
+    check(ctx_, nas_upload_traffic_csr(ctx_, row_ptr.data(), peer_node.data(),
+                                       lat_f32_ ? (const void *)weight_f.data() : weight.data(),
+                                       lat_f32_ ? NAS_DT_F32 : NAS_DT_I32, P, n,
+                                       (int64_t)peer_node.size()),
           "nas_upload_traffic_csr");
     std::vector<int32_t> node_out(P);
     check(ctx_, nas_place(ctx_, node_out.data(), nullptr, nullptr), "nas_place");

@@ -114,9 +114,12 @@ public:
 
     // Network-aware placement of every queued pod (north star): returns
     // (pod, node or "" when nothing fits) in queue order, binding each placed pod.
-    std::vector<std::pair<Pod, Outcome>> place_pending(int dtype = 1 /* NAS_DT_I8 */);
+    // costs on the latency set last: int8 ms (set_latency, exact integer
+    // scores) or fp32 us (set_latency_f32, unquantised measurements)
+    std::vector<std::pair<Pod, Outcome>> place_pending();
     // pairwise latency matrix for place_pending, indexed like `names`
     void set_latency(const std::vector<std::string> &names, const std::vector<int8_t> &L);
+    void set_latency_f32(const std::vector<std::string> &names, const std::vector<float> &L);
 
     void set_topology(std::vector<Endpoint> t) { topo_ = std::move(t); }
     // replaces the reference's node -> report map (:505-510) entry by entry
@@ -144,8 +147,11 @@ private:
     std::map<std::string, std::string> iperf_;
     bool use_ref_iperf_ = true;
     std::vector<NodeMetrics> metrics_;
+    std::vector<int32_t> pod_snap_;  // vote(): every pod on snapshot 0
     std::vector<std::string> lat_names_;
     std::vector<int8_t> lat_;
+    std::vector<float> lat_f_;
+    bool lat_f32_ = false;  // place_pending on lat_f_ (NAS_DT_F32)
 };
 
 }  // namespace nas_host

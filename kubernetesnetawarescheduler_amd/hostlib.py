@@ -66,12 +66,16 @@ SIGNATURES = {
     "nas_host_latency_matrix": (_c.c_int, [_c.c_int32, _c.POINTER(_c.c_char_p),
                                            _c.POINTER(_c.c_size_t), _c.c_void_p]),
     "nas_host_latency_from_bps": (_c.c_int32, [_c.c_double]),
+    "nas_host_latency_matrix_us": (_c.c_int, [_c.c_int32, _c.POINTER(_c.c_char_p),
+                                              _c.POINTER(_c.c_size_t), _c.c_void_p]),
+    "nas_host_latency_us_from_bps": (_c.c_float, [_c.c_double]),
     "nas_host_create": (_c.c_int, [_c.POINTER(_P), _P, _c.POINTER(HostIO)]),
     "nas_host_destroy": (None, [_P]),
     "nas_host_last_error": (_c.c_char_p, [_P]),
     "nas_host_set_topology": (_c.c_int, [_P, _c.POINTER(_CS), _c.POINTER(_CS), _c.c_int32]),
     "nas_host_set_iperf_path": (_c.c_int, [_P, _CS, _CS]),
     "nas_host_set_latency": (_c.c_int, [_P, _c.POINTER(_CS), _c.c_void_p, _c.c_int32]),
+    "nas_host_set_latency_f32": (_c.c_int, [_P, _c.POINTER(_CS), _c.c_void_p, _c.c_int32]),
     "nas_host_enqueue": (_c.c_int, [_P, _c.POINTER(HostPod)]),
     "nas_host_queued": (_c.c_int32, [_P]),
     "nas_host_schedule_one": (_c.c_int, [_P, _c.POINTER(HostOutcome)]),
@@ -141,14 +145,20 @@ def latency_from_bps(bps):
     return hostlib().nas_host_latency_from_bps(float(bps))
 
 
-def latency_matrix(reports):
-    """reports: n x n list of bytes/None (client i -> server j)."""
+def latency_us_from_bps(bps):
+    return hostlib().nas_host_latency_us_from_bps(float(bps))
+
+
+def latency_matrix(reports, us=False):
+    """reports: n x n list of bytes/None (client i -> server j).  int8 ms, or
+    (us=True) float32 microseconds per MB for the fp32 path."""
     n = len(reports)
     flat = [None if reports[i][j] is None else _b(reports[i][j]) for i in range(n) for j in range(n)]
     arr = (_c.c_char_p * (n * n))(*flat)
     lens = (_c.c_size_t * (n * n))(*[0 if x is None else len(x) for x in flat])
-    L = np.zeros((n, n), np.int8)
-    rc = hostlib().nas_host_latency_matrix(n, arr, lens, L.ctypes.data_as(_c.c_void_p))
+    L = np.zeros((n, n), np.float32 if us else np.int8)
+    fn = hostlib().nas_host_latency_matrix_us if us else hostlib().nas_host_latency_matrix
+    rc = fn(n, arr, lens, L.ctypes.data_as(_c.c_void_p))
     if rc != 0:
         raise NasError(rc, "nas_host_latency_matrix")
     return L
@@ -280,10 +290,14 @@ class HostScheduler:
         self._ck(self._L.nas_host_set_iperf_path(self._h, _b(node), _b(path)))
 
     def set_latency(self, names, L):
-        L = np.ascontiguousarray(L, np.int8)
+        """int8 ms (exact integer scores) or float32 us (fp32 costs): the
+        dtype of L picks the path of place_pending."""
+        f32 = np.asarray(L).dtype == np.float32
+        L = np.ascontiguousarray(L, np.float32 if f32 else np.int8)
         n = len(names)
         a = (_CS * n)(*[_b(x) for x in names])
-        self._ck(self._L.nas_host_set_latency(self._h, a, L.ctypes.data_as(_c.c_void_p), n))
+        fn = self._L.nas_host_set_latency_f32 if f32 else self._L.nas_host_set_latency
+        self._ck(fn(self._h, a, L.ctypes.data_as(_c.c_void_p), n))
 
     def enqueue(self, ns, name, uid="", scheduler_name="netAwareScheduler", node_name="",
                 cpu_milli=0, mem_kib=0, peers=()):

@@ -68,8 +68,10 @@ def csr_to_dense(row_ptr, peer_node, weight, N):
     exact (int64 sums, no saturation; unbound peers, node -1, are skipped) --
     for oracle checks."""
     P = len(row_ptr) - 1
-    WA = np.zeros((P, N), np.int64)
+    w = np.asarray(weight)
+    dt = np.float64 if w.dtype.kind == "f" else np.int64  # float weights: fp64 sums
+    WA = np.zeros((P, N), dt)
     rows = np.repeat(np.arange(P), np.diff(row_ptr))
     keep = (peer_node >= 0) & (peer_node < N)
-    np.add.at(WA, (rows[keep], peer_node[keep]), np.asarray(weight)[keep].astype(np.int64))
+    np.add.at(WA, (rows[keep], peer_node[keep]), w[keep].astype(dt))
     return WA

@@ -268,6 +268,23 @@ static void cost_row_bf16(int N, const uint16_t *wa_row, const uint16_t *L, doub
     }
 }
 
+/* one cost row, fp32 inputs: double accumulation (products of two floats are
+ * exact in double; the sum's rounding is ~1e-16 relative) */
+static void cost_row_f32(int N, const float *wa_row, const float *L, double *out) {
+    for (int n = 0; n < N; ++n) out[n] = 0.0;
+    for (int m = 0; m < N; ++m) {
+        double w = wa_row[m];
+        if (w == 0.0) continue;
+        const float *lr = L + (size_t)m * N;
+        for (int n = 0; n < N; ++n) out[n] += w * (double)lr[n];
+    }
+}
+
+void or_cost_f32(int P, int N, const float *WA, const float *L, double *cost) {
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int p = 0; p < P; ++p) cost_row_f32(N, WA + (size_t)p * N, L, cost + (size_t)p * N);
+}
+
 void or_cost_i8(int P, int N, const int32_t *WA, const int8_t *L, int64_t *cost) {
 #pragma omp parallel for schedule(dynamic, 4)
     for (int p = 0; p < P; ++p) cost_row_i8(N, WA + (size_t)p * N, L, cost + (size_t)p * N);
@@ -330,7 +347,7 @@ void or_topk(int P, int N, int k, const int64_t *cost_i, const double *cost_d,
  * updated in place.  Cost rows are computed in parallel blocks (they do not
  * depend on capacity); the commit walk is strictly sequential in pod order.
  * dtype: 1 = int32 traffic x int8 latency (exact int64 costs), 2 = bf16
- * (double costs).
+ * (double costs), 3 = fp32 (double costs).
  */
 int or_place(int P, int N, int dtype, const void *WA, const void *L, const int32_t *rc,
              const int32_t *rm, const int32_t *rp, int32_t *fc, int32_t *fm, int32_t *fp,
@@ -339,7 +356,7 @@ int or_place(int P, int N, int dtype, const void *WA, const void *L, const int32
     int64_t *ci = NULL;
     double *cd = NULL;
     if (dtype == 1) ci = (int64_t *)malloc(sizeof(int64_t) * (size_t)B * N);
-    else if (dtype == 2) cd = (double *)malloc(sizeof(double) * (size_t)B * N);
+    else if (dtype == 2 || dtype == 3) cd = (double *)malloc(sizeof(double) * (size_t)B * N);
     else return -1;
     for (int p0 = 0; p0 < P; p0 += B) {
         int nb = P - p0 < B ? P - p0 : B;
@@ -347,6 +364,8 @@ int or_place(int P, int N, int dtype, const void *WA, const void *L, const int32
         for (int i = 0; i < nb; ++i) {
             if (ci) cost_row_i8(N, (const int32_t *)WA + (size_t)(p0 + i) * N, (const int8_t *)L,
                                 ci + (size_t)i * N);
+            else if (dtype == 3) cost_row_f32(N, (const float *)WA + (size_t)(p0 + i) * N,
+                                              (const float *)L, cd + (size_t)i * N);
             else cost_row_bf16(N, (const uint16_t *)WA + (size_t)(p0 + i) * N,
                                (const uint16_t *)L, cd + (size_t)i * N);
         }

@@ -93,6 +93,25 @@ def vote_batch(snap, order1, order2, pod_snapshot=None):
     return best, win
 
 
+def vote_gomap(snap):
+    """The reference loop over Go-style maps (gomap.cpp): snap = dict of
+    (P, n) arrays, one snapshot per pod.  Returns best[P], order1 (P, n) and
+    order2 (P, n+1) -- the map orders walked -- and (fill_ns, loop_ns)."""
+    cpu = _c(snap["cpu"], np.float64)
+    P, n = cpu.shape
+    arrs = [cpu, _c(snap["mem"], np.float64), _c(snap["rx"], np.int64),
+            _c(snap["tx"], np.int64), _c(snap["bw"], np.float64), _c(snap["disk"], np.int64)]
+    best = np.zeros(P, np.int32)
+    o1 = np.zeros((P, n), np.int32)
+    o2 = np.zeros((P, n + 1), np.int32)
+    fill, loop = ctypes.c_int64(0), ctypes.c_int64(0)
+    rc = lib().or_vote_gomap(n, P, *[_ptr(a) for a in arrs], _ptr(best), _ptr(o1), _ptr(o2),
+                             ctypes.byref(fill), ctypes.byref(loop))
+    if rc:
+        raise ValueError("gomap: priorities map lacks the none key")
+    return best, o1, o2, (fill.value, loop.value)
+
+
 def fit_mask(req, free):
     """req: (P,3) int32 [cpu_milli, mem_kib, pods]; free: (N,3). Returns uint32 (P, ceil(N/32))."""
     req = _c(req, np.int32)
@@ -116,11 +135,15 @@ def _i32(WA):
 
 def cost(WA, L, dtype):
     """dtype 'i8': integer traffic (any int32, never saturated) x int8 latency
-    -> exact int64; 'bf16': uint16 bf16 bits -> float64."""
+    -> exact int64; 'bf16': uint16 bf16 bits -> float64; 'f32': float32 ->
+    float64 (exact products, fp64 sums)."""
     P, N = WA.shape
     if dtype == "i8":
         out = np.zeros((P, N), np.int64)
         lib().or_cost_i8(P, N, _ptr(_i32(WA)), _ptr(_c(L, np.int8)), _ptr(out))
+    elif dtype == "f32":
+        out = np.zeros((P, N), np.float64)
+        lib().or_cost_f32(P, N, _ptr(_c(WA, np.float32)), _ptr(_c(L, np.float32)), _ptr(out))
     else:
         out = np.zeros((P, N), np.float64)
         lib().or_cost_bf16(P, N, _ptr(_c(WA, np.uint16)), _ptr(_c(L, np.uint16)), _ptr(out))
@@ -155,6 +178,10 @@ def place(WA, L, req, free, dtype):
         dt, wa, ll = 1, _i32(WA), _c(L, np.int8)
         ci = np.zeros(P, np.int64)
         cd = None
+    elif dtype == "f32":
+        dt, wa, ll = 3, _c(WA, np.float32), _c(L, np.float32)
+        ci = None
+        cd = np.zeros(P, np.float64)
     else:
         dt, wa, ll = 2, _c(WA, np.uint16), _c(L, np.uint16)
         ci = None

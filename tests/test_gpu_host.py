@@ -156,3 +156,41 @@ def test_place_pending_matches_oracle():
         else:
             assert kind == "BOUND" and node == nodes[w]
     assert (want < 0).any() and (want >= 0).any()
+
+
+def test_place_pending_f32_measured_latency():
+    """The fp32 path end to end: iperf reports -> unquantised microseconds per
+    MB (nas_host_latency_matrix_us) -> NAS_DT_F32 placement of the queued pods;
+    equal to the fp64 sequential oracle on the same float L / traffic."""
+    rng = np.random.default_rng(11)
+    n, P = 48, 200
+    nodes = [f"node{i}" for i in range(n)]
+    bps = rng.uniform(8e7, 2e9, (n, n))
+    reports = [[None if i == j else iperf_report(bps[i, j]) for j in range(n)] for i in range(n)]
+    L = H.latency_matrix(reports, us=True)
+    assert L.dtype == np.float32
+    cap = {nd: (int(rng.integers(500, 2000)), int(rng.integers(400_000, 2_000_000)), 3)
+           for nd in nodes}
+    bound = {f"ns/srv{i}": nodes[int(rng.integers(0, n))] for i in range(40)}
+    cl = H.FakeCluster(nodes=nodes, capacity=cap, bound=dict(bound))
+    pods = []
+    for p in range(P):
+        peers = [(f"ns/srv{int(rng.integers(0, 40))}", int(rng.integers(1, 400)))
+                 for _ in range(int(rng.integers(1, 6)))]
+        pods.append((f"p{p}", int(rng.integers(1, 540)), int(rng.integers(7_464, 303_749)), peers))
+    with Engine(0) as e:
+        s = H.HostScheduler(e, cl)
+        s.set_latency(nodes, L)  # float32: the fp32 path
+        for name, c, m, peers in pods:
+            s.enqueue("ns", name, cpu_milli=c, mem_kib=m, peers=peers)
+        out = s.place_pending()
+    WA = np.zeros((P, n), np.float64)
+    for p, (_, _, _, peers) in enumerate(pods):
+        for q, w in peers:
+            WA[p, nodes.index(bound[q])] += w
+    free = np.array([cap[nd] for nd in nodes], np.int32)
+    req = np.array([[c, m, 1] for _, c, m, _ in pods], np.int32)
+    want, _, _ = oracle.place(WA.astype(np.float32), L, req, free, "f32")
+    got = [nodes.index(node) if kind == "BOUND" else -1 for kind, _, node, _ in out]
+    assert got == want.tolist()
+    assert (want < 0).any() and (want >= 0).any()

@@ -37,10 +37,14 @@ def test_place_golden(engine):
     assert engine.get_capacity().tolist() == g["free_after"]
 
 
-@pytest.mark.parametrize("P,N", [(1, 1), (3, 5), (300, 70), (257, 129), (1000, 300), (513, 1000)])
-def test_fit_mask(engine, P, N):
+@pytest.mark.parametrize("P,N,cap", [(1, 1, 0.05), (3, 5, 0.05), (300, 70, 0.05), (257, 129, 0.05),
+                                     (1000, 300, 0.05), (513, 1000, 0.05), (700, 300, 20.0),
+                                     (1100, 1000, 0.3)])
+def test_fit_mask(engine, P, N, cap):
+    """Bit-exact fit words: mostly failing (0.05), every pod fitting every
+    node (20: k_fit's scalar fast path for whole chunks), and a mix (0.3)."""
     rng = np.random.default_rng(P * 7 + N)
-    WA, L, free, req = cluster(rng, P, N, cap_scale=0.05)
+    WA, L, free, req = cluster(rng, P, N, cap_scale=cap)
     upload(engine, WA, L, free, req, "i8")
     got = engine.filter()  # [ceil(N/64)][P] uint64, bit j <-> node 64c + j
     want = oracle.fit_mask(req, free)  # [P][ceil(N/32)] uint32

@@ -80,6 +80,31 @@ def test_pod_snapshot_gather_and_orders_per_snapshot(engine):
     assert (best == want_best).all() and (win == want_win).all()
 
 
+@pytest.mark.parametrize("S", [1, 7])
+def test_orders_per_pod(engine, S):
+    """nas_upload_pod_orders: every pod of a batch carries its own map orders
+    over a shared snapshot (host scheduler.cpp vote(): ONE scrape, P pods)."""
+    rng = np.random.default_rng(50 + S)
+    n, P = 83, 300
+    snaps = [random_snapshot(rng, n, ties=True) for _ in range(S)]
+    o1 = np.stack([rng.permutation(n) for _ in range(P)]).astype(np.int32)
+    o2 = np.stack([rng.permutation(n + 1) for _ in range(P)]).astype(np.int32)
+    ps = rng.integers(0, S, P).astype(np.int32)
+    engine.upload_snapshot(stack_snapshots(snaps))
+    engine.upload_pod_orders(o1, o2)
+    best, win = engine.score_reference(P, pod_snapshot=ps)
+    for p in range(P):
+        b, w, _ = oracle.vote(snaps[ps[p]], o1[p], o2[p])
+        assert best[p] == b and win[p].tolist() == list(w), p
+    from kubernetesnetawarescheduler_amd import NasError
+    with pytest.raises(NasError):  # the sets belong to exactly P pods
+        engine.score_reference(P - 1, pod_snapshot=ps[:-1])
+    if S == 1:  # per-snapshot sets again replace them
+        engine.upload_orders(o1[0], o2[0])
+        best, _ = engine.score_reference(P, pod_snapshot=ps)
+        assert (best == oracle.vote(snaps[0], o1[0], o2[0])[0]).all()
+
+
 def test_edge_values(engine):
     """NaN metrics, signed zeros, sentinel-equal values, all-zero (Atoi failure) rows."""
     n = 7

@@ -225,6 +225,30 @@ def test_latency_matrix_pairs():
     assert (L == want).all() and (L == L.T).all() and (np.diag(L) == 0).all()
 
 
+@pytest.mark.parametrize("bps,us", [(1e8, 80000.0), (8e9, 1000.0), (1e12, 8.0),
+                                    (0.0, 1e7), (-1.0, 1e7), (float("nan"), 1e7),
+                                    (float("inf"), 0.0), (1.0, 1e7)])
+def test_latency_us_from_bps(bps, us):
+    assert H.latency_us_from_bps(bps) == np.float32(us)
+
+
+def test_latency_matrix_us_unquantised():
+    """The fp32 path keeps the measurement: 8e12 / bps microseconds per MB as
+    float, the slower direction, 1e7 us for unusable pairs."""
+    n = 5
+    rng = np.random.default_rng(2)
+    bps = rng.uniform(5e7, 2e9, (n, n))
+    reports = [[None if i == j else iperf_report(bps[i, j]) for j in range(n)] for i in range(n)]
+    reports[1][4] = "{broken"
+    L = H.latency_matrix(reports, us=True)
+    d = (8e12 / bps).astype(np.float32)
+    d[1, 4] = 1e7
+    want = np.maximum(d, d.T)
+    np.fill_diagonal(want, 0)
+    assert L.dtype == np.float32 and (L == want).all()
+    assert len(np.unique(L[L > 0])) > n  # not quantised to a few levels
+
+
 def test_host_abi_symbols():
     """Every symbol include/nas_host.h declares is exported and bound."""
     import os

@@ -135,3 +135,19 @@ def test_topk_matches_sort():
         order = sorted(fit, key=lambda n: (cost[p, n], n))[:4]
         assert cnt[p] == len(order)
         assert nodes[p, :cnt[p]].tolist() == order
+
+
+def test_gomap_loop_equals_literal_on_its_orders():
+    """The Go-map restatement (bench's reference-mode CPU baseline) returns the
+    map orders it walked; the literal loop on those orders gives the same
+    decision for every pod."""
+    rng = np.random.default_rng(5)
+    snaps = [random_snapshot(rng, 40, ties=bool(i % 2)) for i in range(30)]
+    batch = {k: np.stack([s[k] for s in snaps]) for k in snaps[0]}
+    best, o1, o2, (fill, loop) = oracle.vote_gomap(batch)
+    assert fill > 0 and loop > 0
+    for p, s in enumerate(snaps):
+        assert sorted(o1[p].tolist()) == list(range(40))
+        assert sorted(o2[p].tolist()) == list(range(41))
+        b, _, _ = oracle.vote(s, o1[p], o2[p])
+        assert b == best[p], p
