@@ -6,28 +6,24 @@
 // req[r][p] <= free[r][n] for r in {cpu millicores, memory KiB, pod slots}.
 //
 // Layout: lane-per-NODE.  Each wave owns one 64-node chunk c (lane j = node
-// 64c + j, its three free capacities in VGPRs, read once) and walks pods:
-// a pod's requests are wave-uniform (wide scalar loads of 64 pods at a
-// time), three v_cmp against
-// the lanes' capacities and their AND are the pod's 64-bit fit word for the
-// chunk directly -- the ballot -- which v_writelane drops into lane i of the
-// group's result, so 64 pods end in one coalesced 8-byte-per-lane store:
+// 64c + j, its three free capacities in VGPRs, read once, plus the chunk's
+// minima and maxima, wave-uniform) and walks its pods 64 at a time, lane i
+// holding pod i's requests:
+//   * three v_cmp against the chunk minima decide, for all 64 pods at once,
+//     the pods that fit EVERY valid node of the chunk (word = valid-node
+//     mask), three against the maxima the pods that fit NONE (word = 0);
+//   * each remaining pod is broadcast (v_readlane) and compared against the
+//     64 lanes' capacities: three ballots ANDed are its word, written
+//     into its lane;
+// and the 64 words leave in one coalesced 8-byte-per-lane store:
 //   mask[c * Pp + p]  bit j  <=>  pod p fits local node 64c + j.
-// ~8 instructions per (pod, 64 nodes) instead of ~6 per (pod, node) in a
-// lane-per-pod form.  Most pods fit every node of a chunk outright (requests
-// are small against node capacity until nodes fill up): a pod whose three
-// requests are <= the chunk's smallest capacities (wave-uniform, reduced
-// once) is settled by three SCALAR compares into a 64-pod "fits everything"
-// mask, and one v_cndmask per group writes the chunk's valid-node mask for
-// all of them; only the other pods take the ballot path.  The kernel then
-// runs near the rate of its mask write (P*N/8 bytes, HBM) -- see DESIGN.md.
+// Requests are small against node capacity until nodes fill up, so most
+// (pod, chunk) pairs cost 1/64 of a compare; the kernel runs near the rate of
+// its mask write (P*N/8 bytes, HBM) -- see DESIGN.md.
 #include "nas_internal.h"
 
 namespace nas {
 namespace {
-
-// 16 ints at 4-byte alignment: one s_load_dwordx16 from a uniform address
-typedef int v16i_a4 __attribute__((ext_vector_type(16), aligned(4)));
 
 constexpr int FIT_THREADS = 256;  // 4 waves = 4 node chunks per block
 constexpr int FIT_WAVES = FIT_THREADS / 64;
@@ -64,66 +60,59 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
         fm = __hip_atomic_load(cp + N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         fp = __hip_atomic_load(cp + 2 * (size_t)N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // the chunk's valid nodes and its smallest capacities (padding lanes
-    // excluded: they fit nothing), wave-uniform
-    const unsigned long long valid = __builtin_amdgcn_ballot_w64(nl < nloc);
-    int mc = nl < nloc ? fc : 0x7fffffff, mm = nl < nloc ? fm : 0x7fffffff;
-    int mp = nl < nloc ? fp : 0x7fffffff;
+    // the chunk's valid nodes, its smallest and largest capacities (padding
+    // lanes excluded: they fit nothing), wave-uniform
+    const bool real = nl < nloc;
+    const unsigned long long valid = __builtin_amdgcn_ballot_w64(real);
+    int mc = real ? fc : 0x7fffffff, mm = real ? fm : 0x7fffffff, mp = real ? fp : 0x7fffffff;
+    int xc = real ? fc : (int)0x80000000, xm = real ? fm : (int)0x80000000;
+    int xp = real ? fp : (int)0x80000000;
 #pragma unroll
     for (int o = 32; o; o >>= 1) {
         mc = min(mc, __shfl_xor(mc, o));
         mm = min(mm, __shfl_xor(mm, o));
         mp = min(mp, __shfl_xor(mp, o));
+        xc = max(xc, __shfl_xor(xc, o));
+        xm = max(xm, __shfl_xor(xm, o));
+        xp = max(xp, __shfl_xor(xp, o));
     }
-    mc = __builtin_amdgcn_readfirstlane(mc);
-    mm = __builtin_amdgcn_readfirstlane(mm);
-    mp = __builtin_amdgcn_readfirstlane(mp);
     const unsigned vlo = (unsigned)valid, vhi = (unsigned)(valid >> 32);
     const int pend = min(p_end, pb0 + block_pods);
+    // lane i holds pod pb + i's requests (one coalesced load per resource),
+    // the next group's loaded while this one is decided
+    int q = min(pb0 + lane, Pp - 1);
+    int na = req[q], nb = req[Pp + q], nd = req[2 * (size_t)Pp + q];
     for (int pb = pb0; pb < pend; pb += 64) {
-        unsigned lo = 0, hi = 0;
-        unsigned long long all_fit = 0;  // pods of the group that fit every valid node
-        // lane i takes pod pb + i's word: three v_cmp of the pod's (uniform)
-        // requests against the lanes' capacities straight into SGPR lane
-        // masks, ANDed on the scalar unit, v_writelane into lane i
-        auto pod = [&](int i, int ra, int rb, int rd) {
-            if (ra <= mc && rb <= mm && rd <= mp) {  // uniform: scalar compares only
-                all_fit |= 1ull << i;
-                return;
-            }
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(ra <= fc) &
-                                         __builtin_amdgcn_ballot_w64(rb <= fm) &
-                                         __builtin_amdgcn_ballot_w64(rd <= fp);
-            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(lo) : "s"((unsigned)m), "i"(i));
-            asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(hi) : "s"((unsigned)(m >> 32)), "i"(i));
-        };
-        if (pb + 64 <= Pp) {
-            // the group's requests through the scalar unit: wide s_loads of
-            // 64 consecutive ints per resource, issued together
-            const int *qa = req + pb, *qb = req + Pp + pb, *qd = req + 2 * (size_t)Pp + pb;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const v16i_a4 a = *reinterpret_cast<const v16i_a4 *>(qa + 16 * k);
-                const v16i_a4 b = *reinterpret_cast<const v16i_a4 *>(qb + 16 * k);
-                const v16i_a4 d = *reinterpret_cast<const v16i_a4 *>(qd + 16 * k);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) pod(16 * k + i, a[i], b[i], d[i]);
-            }
-        } else {
-            // a window running past the padded rows (rescore views): one
-            // coalesced load per resource, broadcast with v_readlane
-            const int q = min(pb + lane, Pp - 1);
-            const int va = req[q], vb = req[Pp + q], vd = req[2 * Pp + q];
-#pragma unroll
-            for (int i = 0; i < 64; ++i)
-                pod(i, __builtin_amdgcn_readlane(va, i), __builtin_amdgcn_readlane(vb, i),
-                    __builtin_amdgcn_readlane(vd, i));
+        const int ra = na, rb = nb, rd = nd;
+        if (pb + 64 < pend) {
+            q = min(pb + 64 + lane, Pp - 1);
+            na = req[q];
+            nb = req[Pp + q];
+            nd = req[2 * (size_t)Pp + q];
         }
-        if ((all_fit >> lane) & 1) {
-            lo = vlo;
-            hi = vhi;
+        const bool in = pb + lane < pend;
+        // 64 pods at once against the chunk's extremes: fits every valid node
+        // (requests <= the minima) or none (some request > its maximum)
+        const unsigned long long all = __builtin_amdgcn_ballot_w64(in && ra <= mc && rb <= mm && rd <= mp);
+        const unsigned long long none = __builtin_amdgcn_ballot_w64(in && (ra > xc || rb > xm || rd > xp));
+        unsigned long long rest = __builtin_amdgcn_ballot_w64(in) & ~all & ~none;
+        unsigned lo = ((all >> lane) & 1) ? vlo : 0u, hi = ((all >> lane) & 1) ? vhi : 0u;
+        // the others one by one: the pod's (broadcast) requests against the
+        // lanes' capacities, three ballots ANDed, written into its lane
+        while (rest) {
+            const int i = (int)__builtin_ctzll(rest);
+            rest &= rest - 1;
+            const int a = __builtin_amdgcn_readlane(ra, i), b = __builtin_amdgcn_readlane(rb, i);
+            const int d = __builtin_amdgcn_readlane(rd, i);
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(a <= fc) &
+                                         __builtin_amdgcn_ballot_w64(b <= fm) &
+                                         __builtin_amdgcn_ballot_w64(d <= fp);
+            if (lane == i) {
+                lo = (unsigned)m;
+                hi = (unsigned)(m >> 32);
+            }
         }
-        if (pb + lane < pend) mask[(size_t)c * Pp + pb + lane] = ((unsigned long long)hi << 32) | lo;
+        if (in) mask[(size_t)c * Pp + pb + lane] = ((unsigned long long)hi << 32) | lo;
     }
 }
 

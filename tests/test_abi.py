@@ -75,3 +75,22 @@ def test_missing_library_fails_loudly(monkeypatch):
     monkeypatch.setattr(_lib, "LIB_PATH", os.path.join(ROOT, "no_such_dir", "libnas.so"))
     with pytest.raises(_lib.NasError, match="not built"):
         _lib.lib()
+
+
+def test_go_binding_uses_declared_abi():
+    """scheduler/nas.go (the cgo binding for the reference's package main):
+    every C.nas_* call and C.NAS_* constant it names is in include/nas.h, and
+    the config field it sets exists (the Go toolchain is absent here)."""
+    with open(os.path.join(ROOT, "scheduler", "nas.go")) as f:
+        go = f.read()
+    with open(os.path.join(ROOT, "include", "nas.h")) as f:
+        hdr = f.read()
+    funcs = set(re.findall(r"\bC\.(nas_[a-z0-9_]+)\(", go))
+    assert funcs and funcs <= set(declared()), funcs - set(declared())
+    L = _lib.lib()
+    assert all(hasattr(L, n) for n in funcs)
+    consts = set(re.findall(r"\bC\.(NAS_[A-Z0-9_]+)\b", go))
+    defined = set(re.findall(r"#define\s+(NAS_[A-Z0-9_]+)", hdr))
+    assert consts and consts <= defined, consts - defined
+    assert set(re.findall(r"\bC\.(nas_[a-z_]+)\{", go)) <= {"nas_config"}
+    assert re.search(r"int32_t\s+device\s*;", hdr)
