@@ -4,6 +4,7 @@
 // loop.  Every entry re-binds the context's device and synchronises its
 // stream before returning (blocking semantics of the Go call it replaces).
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <chrono>
@@ -17,6 +18,18 @@
 
 using nas::DevBuf;
 using nas::KC;
+
+// roctx range around every C-ABI entry (rocprofv3 --marker-trace shows the
+// host call that issued each kernel); a no-op call without a profiler
+namespace {
+struct RoctxRange {
+    explicit RoctxRange(const char *name) { roctxRangePush(name); }
+    ~RoctxRange() { roctxRangePop(); }
+    RoctxRange(const RoctxRange &) = delete;
+    RoctxRange &operator=(const RoctxRange &) = delete;
+};
+}  // namespace
+#define NAS_RANGE(name) const RoctxRange nas_range_(name)
 
 namespace nas {
 
@@ -788,6 +801,7 @@ extern "C" {
 int nas_version(void) { return NAS_ABI_VERSION; }
 
 int nas_create(nas_ctx **out, const nas_config *cfg) {
+    NAS_RANGE("nas_create");
     if (!out) return NAS_ERR_ARG;
     *out = nullptr;
     int ndev = 0;
@@ -815,6 +829,7 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
 }
 
 void nas_destroy(nas_ctx *ctx) {
+    NAS_RANGE("nas_destroy");
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream_commit}) (void)hipStreamSynchronize(st);
@@ -930,6 +945,7 @@ int prepare_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, i
 int nas_upload_snapshot(nas_ctx *ctx, const double *cpu, const double *mem, const int64_t *rx,
                         const int64_t *tx, const double *bw, const int64_t *disk, int32_t n_nodes,
                         int32_t n_snapshots) {
+    NAS_RANGE("nas_upload_snapshot");
     OK(bind(ctx));
     return upload_snapshot_slice(ctx, cpu, mem, rx, tx, bw, disk, n_nodes, 0, n_nodes, n_snapshots,
                                  false);
@@ -939,6 +955,7 @@ int nas_upload_snapshot_shard(nas_ctx *ctx, const double *cpu, const double *mem
                               const int64_t *rx, const int64_t *tx, const double *bw,
                               const int64_t *disk, int32_t n_nodes, int32_t node_lo,
                               int32_t n_local, int32_t n_snapshots) {
+    NAS_RANGE("nas_upload_snapshot_shard");
     OK(bind(ctx));
     return upload_snapshot_slice(ctx, cpu, mem, rx, tx, bw, disk, n_nodes, node_lo, n_local,
                                  n_snapshots, true);
@@ -946,6 +963,7 @@ int nas_upload_snapshot_shard(nas_ctx *ctx, const double *cpu, const double *mem
 
 int nas_vote_partials(nas_ctx *ctx, const int32_t *order1, const int32_t *order2, int32_t S,
                       nas_vote_partial *out) {
+    NAS_RANGE("nas_vote_partials");
     OK(bind(ctx));
     OK(prepare_orders(ctx, order1, order2, S));
     if (S < 0 || S > ctx->snap_s || (S > 0 && !out))
@@ -970,6 +988,7 @@ int nas_vote_partials(nas_ctx *ctx, const int32_t *order1, const int32_t *order2
 
 int nas_vote_merge(nas_ctx *ctx, const nas_vote_partial *parts, int32_t n_parts, int32_t S,
                    int32_t *best_out, int32_t *winners_out) {
+    NAS_RANGE("nas_vote_merge");
     OK(bind(ctx));
     OK(prepare_orders(ctx, nullptr, nullptr, 1));
     if (n_parts < 1 || S < 0 || (S > 0 && (!parts || !best_out)))
@@ -1007,12 +1026,14 @@ int nas_vote_merge(nas_ctx *ctx, const nas_vote_partial *parts, int32_t n_parts,
 
 int nas_upload_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
                       int32_t n_orders) {
+    NAS_RANGE("nas_upload_orders");
     OK(bind(ctx));
     return upload_orders(ctx, order1, order2, n_orders);
 }
 
 int nas_upload_pod_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
                           int32_t n_pods) {
+    NAS_RANGE("nas_upload_pod_orders");
     OK(bind(ctx));
     return upload_orders(ctx, order1, order2, n_pods, true);
 }
@@ -1020,6 +1041,7 @@ int nas_upload_pod_orders(nas_ctx *ctx, const int32_t *order1, const int32_t *or
 int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *order2,
                         const int32_t *pod_snapshot, int32_t P, int32_t *best_out,
                         int32_t *winners_out) {
+    NAS_RANGE("nas_score_reference");
     OK(bind(ctx));
     if (ctx->snap_s <= 0) return nas::fail(ctx, NAS_ERR_STATE, "no snapshot uploaded");
     if (P < 0 || (P > 0 && !best_out)) return nas::fail(ctx, NAS_ERR_ARG, "P / best_out");
@@ -1126,6 +1148,7 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
 
 // ----------------------------------------------------------------- extended
 int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
+    NAS_RANGE("nas_upload_latency");
     OK(bind(ctx));
     if (!L || n <= 0 || !valid_dtype(dtype))
         return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_latency: L / n / dtype");
@@ -1164,6 +1187,7 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
 
 int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *mem_kib,
                         const int32_t *pods, int32_t n) {
+    NAS_RANGE("nas_upload_capacity");
     OK(bind(ctx));
     if (!cpu_milli || !mem_kib || !pods || n <= 0)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_capacity");
@@ -1185,6 +1209,7 @@ int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *m
 }
 
 int nas_reset_capacity(nas_ctx *ctx) {
+    NAS_RANGE("nas_reset_capacity");
     OK(bind(ctx));
     if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
     HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)ctx->B * 3 * ctx->cap_n * 4,
@@ -1195,6 +1220,7 @@ int nas_reset_capacity(nas_ctx *ctx) {
 
 int nas_get_capacity(nas_ctx *ctx, int32_t *cpu_milli, int32_t *mem_kib, int32_t *pods,
                      int32_t n) {
+    NAS_RANGE("nas_get_capacity");
     OK(bind(ctx));
     if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
     if (n != ctx->cap_n || !cpu_milli || !mem_kib || !pods)
@@ -1210,6 +1236,7 @@ int nas_get_capacity(nas_ctx *ctx, int32_t *cpu_milli, int32_t *mem_kib, int32_t
 
 int nas_upload_pods(nas_ctx *ctx, const int32_t *rc, const int32_t *rm, const int32_t *rp,
                     int32_t P) {
+    NAS_RANGE("nas_upload_pods");
     OK(bind(ctx));
     if (!rc || !rm || !rp || P <= 0) return nas::fail(ctx, NAS_ERR_ARG, "nas_upload_pods");
     const size_t B = ctx->B;
@@ -1261,6 +1288,7 @@ static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
 }
 
 int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_t P, int32_t n) {
+    NAS_RANGE("nas_upload_traffic_dense");
     OK(bind(ctx));
     if (!WA) return nas::fail(ctx, NAS_ERR_ARG, "WA null");
     if (dtype == NAS_DT_I32) {
@@ -1311,6 +1339,7 @@ int nas_upload_traffic_dense(nas_ctx *ctx, const void *WA, int32_t dtype, int32_
 
 int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *peer_node,
                            const void *weight, int32_t dtype, int32_t P, int32_t n, int64_t nnz) {
+    NAS_RANGE("nas_upload_traffic_csr");
     OK(bind(ctx));
     if (!row_ptr || nnz < 0 || (nnz > 0 && (!peer_node || !weight)))
         return nas::fail(ctx, NAS_ERR_ARG, "csr arrays");
@@ -1464,6 +1493,7 @@ int nas_upload_traffic_csr(nas_ctx *ctx, const int32_t *row_ptr, const int32_t *
 }
 
 int nas_filter(nas_ctx *ctx, uint64_t *mask_out) {
+    NAS_RANGE("nas_filter");
     OK(bind(ctx));
     OK(no_batch(ctx, "nas_filter"));
     if (!ctx->have_cap || !ctx->have_pods || ctx->N <= 0)
@@ -1489,6 +1519,7 @@ int nas_filter(nas_ctx *ctx, uint64_t *mask_out) {
 }
 
 int nas_score(nas_ctx *ctx) {
+    NAS_RANGE("nas_score");
     OK(bind(ctx));
     OK(check_extended(ctx));
     OK(alloc_extended(ctx));
@@ -1507,6 +1538,7 @@ int nas_score(nas_ctx *ctx) {
 }
 
 int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_score_out) {
+    NAS_RANGE("nas_place");
     OK(bind(ctx));
     OK(check_extended(ctx));
     if (ctx->virtual_shard)
@@ -1659,6 +1691,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
 
 int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i, float *cand_cost_f,
                        int32_t *count, int32_t *complete) {
+    NAS_RANGE("nas_get_candidates");
     OK(bind(ctx));
     if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
     const int64_t P = (int64_t)ctx->B * ctx->P;  // a batch: B clusters back to back
@@ -1690,6 +1723,7 @@ int nas_get_candidates(nas_ctx *ctx, int32_t *cand_node, int64_t *cand_cost_i, f
 
 // ------------------------------------------------------- host-driven steps
 int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi) {
+    NAS_RANGE("nas_score_range");
     OK(bind(ctx));
     OK(no_batch(ctx, "nas_score_range"));
     OK(check_extended(ctx));
@@ -1719,6 +1753,7 @@ static int keys_range_ok(nas_ctx *ctx, int32_t p_lo, int32_t n, const void *keys
 
 int nas_get_candidate_keys_range(nas_ctx *ctx, int32_t p_lo, int32_t n, uint64_t *keys,
                                  uint64_t *bounds) {
+    NAS_RANGE("nas_get_candidate_keys_range");
     OK(bind(ctx));
     OK(no_batch(ctx, "candidate key ranges"));
     OK(keys_range_ok(ctx, p_lo, n, keys, bounds));
@@ -1733,6 +1768,7 @@ int nas_get_candidate_keys_range(nas_ctx *ctx, int32_t p_lo, int32_t n, uint64_t
 
 int nas_set_candidate_keys(nas_ctx *ctx, int32_t p_lo, int32_t n, const uint64_t *keys,
                            const uint64_t *bounds) {
+    NAS_RANGE("nas_set_candidate_keys");
     OK(bind(ctx));
     OK(no_batch(ctx, "candidate key ranges"));
     OK(check_extended(ctx));
@@ -1761,6 +1797,7 @@ int nas_set_candidate_keys(nas_ctx *ctx, int32_t p_lo, int32_t n, const uint64_t
 
 int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out,
                int64_t *int_score_out, int32_t *stop_out) {
+    NAS_RANGE("nas_commit");
     OK(bind(ctx));
     OK(no_batch(ctx, "nas_commit"));
     OK(check_extended(ctx));
@@ -1812,6 +1849,7 @@ int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out
 
 // ---------------------------------------------------------------- multi-GPU
 int nas_comm_unique_id(uint8_t id_out[128]) {
+    NAS_RANGE("nas_comm_unique_id");
     if (!id_out) return NAS_ERR_ARG;
     ncclUniqueId id;
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
@@ -1821,6 +1859,7 @@ int nas_comm_unique_id(uint8_t id_out[128]) {
 }
 
 int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world) {
+    NAS_RANGE("nas_comm_init");
     OK(bind(ctx));
     if (!id || world < 1 || rank < 0 || rank >= world)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_comm_init: rank/world");
@@ -1859,6 +1898,7 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
 }
 
 int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world) {
+    NAS_RANGE("nas_set_shard");
     OK(bind(ctx));
     if (world < 1 || rank < 0 || rank >= world)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_set_shard: rank/world");
@@ -1874,6 +1914,7 @@ int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world) {
 }
 
 int nas_get_candidate_keys(nas_ctx *ctx, uint64_t *keys, uint64_t *bounds) {
+    NAS_RANGE("nas_get_candidate_keys");
     OK(bind(ctx));
     OK(no_batch(ctx, "nas_get_candidate_keys"));
     if (!ctx->scored) return nas::fail(ctx, NAS_ERR_STATE, "no scoring pass yet");
@@ -1912,18 +1953,21 @@ int synth_snapshot_slice(nas_ctx *ctx, uint64_t seed, int32_t n, int32_t lo, int
 }  // namespace
 
 int nas_synth_snapshots(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t n_snapshots) {
+    NAS_RANGE("nas_synth_snapshots");
     OK(bind(ctx));
     return synth_snapshot_slice(ctx, seed, n_nodes, 0, n_nodes, n_snapshots, false);
 }
 
 int nas_synth_snapshots_shard(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t node_lo,
                               int32_t n_local, int32_t n_snapshots) {
+    NAS_RANGE("nas_synth_snapshots_shard");
     OK(bind(ctx));
     return synth_snapshot_slice(ctx, seed, n_nodes, node_lo, n_local, n_snapshots, true);
 }
 
 int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t *rx, int64_t *tx,
                       double *bw, int64_t *disk) {
+    NAS_RANGE("nas_read_snapshot");
     OK(bind(ctx));
     if (s < 0 || s >= ctx->snap_s) return nas::fail(ctx, NAS_ERR_ARG, "snapshot index");
     void *dst[6] = {cpu, mem, bw, rx, tx, disk};
@@ -1937,6 +1981,7 @@ int nas_read_snapshot(nas_ctx *ctx, int32_t s, double *cpu, double *mem, int64_t
 }
 
 int nas_set_batch(nas_ctx *ctx, int32_t n_clusters) {
+    NAS_RANGE("nas_set_batch");
     OK(bind(ctx));
     if (n_clusters < 1 || n_clusters > 65535)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_set_batch: n_clusters");
@@ -2029,12 +2074,14 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
 
 int nas_synth_cluster(nas_ctx *ctx, uint64_t seed, int32_t n_nodes, int32_t P, int32_t dtype,
                       int32_t peers) {
+    NAS_RANGE("nas_synth_cluster");
     OK(bind(ctx));
     return synth(ctx, seed, 1, n_nodes, P, dtype, peers);
 }
 
 int nas_synth_batch(nas_ctx *ctx, uint64_t seed, int32_t n_clusters, int32_t n_nodes, int32_t P,
                     int32_t dtype, int32_t peers) {
+    NAS_RANGE("nas_synth_batch");
     OK(bind(ctx));
     return synth(ctx, seed, n_clusters, n_nodes, P, dtype, peers);
 }
@@ -2042,6 +2089,7 @@ int nas_synth_batch(nas_ctx *ctx, uint64_t seed, int32_t n_clusters, int32_t n_n
 int nas_read_inputs(nas_ctx *ctx, int32_t p0, int32_t np, void *WA_rows, void *L, int32_t *cap_cpu,
                     int32_t *cap_mem, int32_t *cap_pods, int32_t *req_cpu, int32_t *req_mem,
                     int32_t *req_pods) {
+    NAS_RANGE("nas_read_inputs");
     OK(bind(ctx));
     OK(check_extended(ctx));
     const int N = ctx->N;

@@ -94,3 +94,19 @@ def test_go_binding_uses_declared_abi():
     assert consts and consts <= defined, consts - defined
     assert set(re.findall(r"\bC\.(nas_[a-z_]+)\{", go)) <= {"nas_config"}
     assert re.search(r"int32_t\s+device\s*;", hdr)
+
+
+def test_entries_carry_roctx_ranges():
+    """Every C-ABI entry opens a roctx range (rocprofv3 --marker-trace)."""
+    import shutil
+    import subprocess
+    if shutil.which("nm") is None:
+        pytest.skip("needs nm")
+    und = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert "roctxRangePush" in und and "roctxRangePop" in und
+    with open(os.path.join(ROOT, "kubernetesnetawarescheduler_amd", "csrc", "nas_api.hip")) as f:
+        src = f.read()
+    ranged = set(re.findall(r'NAS_RANGE\("(nas_[a-z0-9_]+)"\)', src))
+    trivial = {"nas_version", "nas_last_error", "nas_get_timings", "nas_set_option"}
+    assert set(declared()) - trivial <= ranged, set(declared()) - trivial - ranged
