@@ -173,12 +173,27 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     const int b = blockIdx.x;
     const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-    const int gsize = GM * n_nt;
-    const int g = v / gsize;
-    const int first_mt = g * GM;
-    const int gm = min(n_mt - first_mt, GM);
-    const int mt = first_mt + (v % gsize) % gm;
-    const int nt = (v % gsize) / gm;
+    int mt, nt;
+    if constexpr (GM > 0) {
+        // node-group major: GM node tiles x every pod tile, pod-minor
+        const int gsize = GM * n_nt;
+        const int g = v / gsize;
+        const int first_mt = g * GM;
+        const int gm = min(n_mt - first_mt, GM);
+        mt = first_mt + (v % gsize) % gm;
+        nt = (v % gsize) / gm;
+    } else {
+        // pod-group major (GM = -PG): PG pod tiles x every node tile, so an
+        // XCD keeps one pod group's traffic rows (PG x 2.5 MB at C3) hot in
+        // the memory-side cache while it sweeps the node tiles
+        constexpr int PG = GM < 0 ? -GM : 1;
+        const int gsize = PG * n_mt;
+        const int g = v / gsize, r = v % gsize;
+        const int first_nt = g * PG;
+        const int pg = min(n_nt - first_nt, PG);
+        mt = r / pg;
+        nt = first_nt + r % pg;
+    }
     const int cb = blockIdx.y;  // cluster of a batched launch
     Lt += (size_t)cb * n_mt * BM * Kb;
     WA += (size_t)cb * Pp * Kb;
@@ -825,6 +840,8 @@ NAS_INST(3, 5, 0, 4) NAS_INST(0, 1, 0, 4) NAS_INST(0, 5, 0, 8) NAS_INST(4, 0, 0,
 NAS_INST(0, 1, 2, 4) NAS_INST(0, 1, 3, 4) NAS_INST(0, 0, 2, 4) NAS_INST(0, 0, 3, 4)
 NAS_INST(1, 1, 2, 4) NAS_INST(1, 1, 3, 4)
 NAS_INST(0, 0, 4, 4) NAS_INST(1, 0, 4, 4) NAS_INST(0, 0, 4, 8) NAS_INST(0, 0, 4, 2)
+NAS_INST(0, 0, 0, -2) NAS_INST(0, 0, 0, -4) NAS_INST(0, 0, 0, -8) NAS_INST(0, 0, 0, 8)
+NAS_INST(0, 0, 0, 2) NAS_INST(0, 0, 0, 16)
 #undef NAS_INST
 
 #endif

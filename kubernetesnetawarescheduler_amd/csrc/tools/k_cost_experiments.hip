@@ -39,7 +39,7 @@ __device__ __forceinline__ v4i gld16(const unsigned char *p) {
 // A lane ends with 128 (node, cost) values of ONE pod, so the top-k needs no
 // cross-wave merge: per-lane top-4, one lane^32 exchange, 72 B per pod.
 // ---------------------------------------------------------------------------
-template <int DT, int EPI = 0, int NST = 4, int GM = COST_GM>
+template <int DT, int EPI = 0, int NST = 4, int GM = COST_GM, bool TB = false>
 __global__ void __launch_bounds__(THREADS, 1)
 k_cost_topk2(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
              int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
@@ -98,9 +98,16 @@ k_cost_topk2(const unsigned char *__restrict__ Lt, const unsigned char *__restri
             glds16(Ag + (size_t)row * Kb + k0 + c * 16, base + r0 * BKB);
         }
     };
+    // TB: WA pre-tiled in MFMA fragment order -- [pod group of 32][K-step]
+    // [substep][64 lanes x 16 B] -- so each load is one contiguous 1 KiB
+    // (8 full lines) instead of 32 rows x 32 B (timing only: same bytes)
+    const unsigned char *Bt = WA + (size_t)(pod_row >> 5) * 32 * Kb + lane * 16;
     auto loadB = [&](v4i (&b)[4], int k0) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) b[s] = *reinterpret_cast<const v4i *>(Bl + k0 + 16 * s);
+        for (int s = 0; s < 4; ++s) {
+            if constexpr (TB) b[s] = *reinterpret_cast<const v4i *>(Bt + k0 * 32 + 1024 * s);
+            else b[s] = *reinterpret_cast<const v4i *>(Bl + k0 + 16 * s);
+        }
     };
 
     // the epilogue's fit-mask words (4 per pod: nodes 64c .. 64c+63 of the tile)
@@ -315,7 +322,7 @@ k_cost_topk2(const unsigned char *__restrict__ Lt, const unsigned char *__restri
 // read while the current MFMAs run, and WA rows streamed two K-steps ahead.
 // ---------------------------------------------------------------------------
 constexpr int THREADS3 = 256;
-template <int DT, int EPI = 0, int NST = 4, int GM = COST_GM>
+template <int DT, int EPI = 0, int NST = 4, int GM = COST_GM, bool TB = false>
 __global__ void __launch_bounds__(THREADS3, 1)
 k_cost_topk3(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
              int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
@@ -375,11 +382,14 @@ k_cost_topk3(const unsigned char *__restrict__ Lt, const unsigned char *__restri
     // WA rows by inline-asm loads retired by the explicit vmcnt of wait_step
     // (a compiler-visible load carried into the next loop iteration makes
     // hipcc put a vmcnt(0) in front of every step, draining the A prefetch)
+    // TB: WA pre-tiled in fragment order (see k_cost_topk2): 1 KiB per load
+    const unsigned char *T0 = WA + (size_t)(prow0 >> 5) * 32 * Kb + lane * 16;
+    const unsigned char *T1 = T0 + (size_t)32 * Kb;
     auto loadB = [&](v4i (&b)[2][4], int k0) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) b[0][s] = gld16(B0 + k0 + 16 * s);
+        for (int s = 0; s < 4; ++s) b[0][s] = gld16(TB ? T0 + k0 * 32 + 1024 * s : B0 + k0 + 16 * s);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) b[1][s] = gld16(B1 + k0 + 16 * s);
+        for (int s = 0; s < 4; ++s) b[1][s] = gld16(TB ? T1 + k0 * 32 + 1024 * s : B1 + k0 + 16 * s);
     };
 
     u64 mw[2][4];
@@ -681,12 +691,24 @@ k_cost_topk3(const unsigned char *__restrict__ Lt, const unsigned char *__restri
 NAS_INST2(0, 4, 4) NAS_INST2(1, 4, 4) NAS_INST2(3, 4, 4) NAS_INST2(4, 4, 4) NAS_INST2(0, 3, 4)
 NAS_INST2(0, 4, 8) NAS_INST2(1, 3, 4)
 #undef NAS_INST2
+#define NAS_INST2T(E, S, G)                                                                        \
+    template __global__ void k_cost_topk2<NAS_DT_I8, E, S, G, true>(                               \
+        const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
+        u64 *, int, const int *, int, const int *, Ovf);
+NAS_INST2T(0, 4, 4) NAS_INST2T(1, 4, 4) NAS_INST2T(0, 3, 4)
+#undef NAS_INST2T
 #define NAS_INST3(E, S, G)                                                                         \
     template __global__ void k_cost_topk3<NAS_DT_I8, E, S, G>(                                     \
         const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
         u64 *, int, const int *, int, const int *, Ovf);
 NAS_INST3(0, 4, 4) NAS_INST3(1, 4, 4) NAS_INST3(3, 4, 4) NAS_INST3(4, 4, 4) NAS_INST3(0, 4, 8)
 #undef NAS_INST3
+#define NAS_INST3T(E, S, G)                                                                        \
+    template __global__ void k_cost_topk3<NAS_DT_I8, E, S, G, true>(                               \
+        const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
+        u64 *, int, const int *, int, const int *, Ovf);
+NAS_INST3T(0, 4, 4) NAS_INST3T(1, 4, 4)
+#undef NAS_INST3T
 #endif
 }  // namespace
 }  // namespace nas

@@ -54,7 +54,15 @@ int main(int argc, char **argv) {
 #define KV3(E, S, G) (const void *)&k_cost_topk3<NAS_DT_I8, E, S, G>, (S) * TILE_BYTES
                       {"v3/top4", KV3(0, 4, 4)}, {"v3/noepi", KV3(1, 4, 4)},
                       {"v3/l2hot", KV3(3, 4, 4)}, {"v3/ldsonly", KV3(4, 4, 4)},
-                      {"v3/top4/g8", KV3(0, 4, 8)}};
+                      {"v3/top4/g8", KV3(0, 4, 8)},
+                      {"top4/podg2", KV(0, 0, 0, -2)}, {"top4/podg4", KV(0, 0, 0, -4)},
+                      {"top4/podg8", KV(0, 0, 0, -8)}, {"top4/g8", KV(0, 0, 0, 8)},
+                      {"top4/g2", KV(0, 0, 0, 2)}, {"top4/g16", KV(0, 0, 0, 16)},
+#define KV2T(E, S, G) (const void *)&k_cost_topk2<NAS_DT_I8, E, S, G, true>, (S) * TILE_BYTES
+#define KV3T(E, S, G) (const void *)&k_cost_topk3<NAS_DT_I8, E, S, G, true>, (S) * TILE_BYTES
+                      {"v2T/top4/st4", KV2T(0, 4, 4)}, {"v2T/noepi/st4", KV2T(1, 4, 4)},
+                      {"v2T/top4/st3", KV2T(0, 3, 4)}, {"v3T/top4", KV3T(0, 4, 4)},
+                      {"v3T/noepi", KV3T(1, 4, 4)}};
     const int nv = sizeof(vars) / sizeof(vars[0]);
     for (int v = 0; v < nv; ++v)
         CK(hipFuncSetAttribute(vars[v].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[v].lds));
@@ -75,7 +83,7 @@ int main(int argc, char **argv) {
             void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero,
                             (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf};
             CK(hipEventRecord(a));
-            const int thr = strncmp(vars[v].name, "v3", 2) ? THREADS : THREADS3;
+            const int thr = strncmp(vars[v].name, "v3", 2) ? THREADS : THREADS3;  // v3 and v3T
             CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(thr), args, vars[v].lds, 0));
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
