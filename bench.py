@@ -61,7 +61,8 @@ def parse():
                     help="diagnostic at --gpus 1: time rank 0 of a G-GPU node-sharded pass "
                          "(its node columns; the other ranks' lists are shifted copies of its "
                          "own; placements not meaningful, RCCL over a one-rank communicator)")
-    ap.add_argument("--only", choices=["place", "vote", "score", "pmc"], default=None,
+    ap.add_argument("--only", choices=["place", "vote", "score", "pmc", "C1", "C2", "C2_f32",
+                                       "C3_bf16", "C5", "C4"], default=None,
                     help="profile helper: run only one path (pmc: the score and vote legs, "
                          "what the in-run PMC passes profile)")
     ap.add_argument("--no-pmc", action="store_true",
@@ -623,12 +624,14 @@ def config_c4(args, d, eng, N=50000, P=500000):
             "stages_ms": {k: res["t"][k] for k in ("fit_ms", "cost_ms", "merge_ms", "commit_ms")}}
 
 
-def run_configs(args, d):
+def run_configs(args, d, only=None):
     """The other BASELINE configs, each on a fresh context (one GPU)."""
     from kubernetesnetawarescheduler_amd import Engine
     out = {}
     for name, fn in (("C1", config_c1), ("C2", config_c2), ("C2_f32", config_c2_f32),
                      ("C3_bf16", config_c3_bf16), ("C5", config_c5), ("C4", config_c4)):
+        if only and name != only:
+            continue
         with Engine(d.local) as e:
             out[name] = fn(args, d, e)
     return out
@@ -666,6 +669,13 @@ def main():
                       "nodes": N, "pods": P, "parallelism": f"node-sharded x{d.world}",
                       "candidates_per_pod": 8}}
     gpu_nodes = None
+    cfg_only = args.only if args.only and args.only.startswith("C") else None
+    if cfg_only:  # one config line alone (profiling)
+        eng.close()
+        out["configs"] = run_configs(args, d, cfg_only)
+        if d.rank == 0:
+            print(json.dumps(out), file=result_out, flush=True)
+        return
     if args.rehearse_world > 1:
         out["rehearsal"] = (f"rank 0 of a {args.rehearse_world}-GPU node-sharded pass on one GPU: "
                             "its node columns scored, the other ranks' lists stood in for by "
