@@ -386,6 +386,9 @@ def cpu_baseline_vote(args, eng, ref):
 
 
 def _timed_place(d, eng, steps, warmup):
+    """Timed placement passes with stage timings off (only the events the
+    pass synchronises on, as in the headline); one more pass with them on
+    fills res["t"] (stages, rescore counts)."""
     res = {}
 
     def step():
@@ -393,7 +396,15 @@ def _timed_place(d, eng, steps, warmup):
         res["node"], _, res["score"] = eng.place(want_cost=True)
         res["t"] = eng.timings()
 
-    return time_steps(d, step, steps, warmup), res
+    for _ in range(warmup):
+        step()
+    eng.set_option("STAGE_TIMINGS", 0)
+    t = time_steps(d, step, steps, 0)
+    eng.set_option("STAGE_TIMINGS", 1)
+    node, score = res["node"].copy(), res["score"].copy()
+    step()
+    assert (res["node"] == node).all() and (res["score"] == score).all()
+    return t, res
 
 
 def config_c1(args, d, eng):

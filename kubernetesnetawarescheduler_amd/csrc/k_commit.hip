@@ -46,6 +46,11 @@ constexpr int THREADS = 1024;  // one window of pods per round
 constexpr int LDS_DYN_MAX = 160 * 1024 - 512;  // leaves room for the static LDS
 constexpr int LDS_CAP_MAX_NODES = LDS_DYN_MAX / 12;
 constexpr int NO_POD = 0x7fffffff;
+// walks of up to this many pods run in one wave (k_commit_w): fewer, exact
+// stops for herds on small clusters (C2: 0.67 -> 0.62 ms per pass); longer
+// walks keep the 1024-pod windows of k_commit, whose conflict-free rounds
+// commit 16x more pods each (C3: 0.8 vs 2.4 ms of commit per pass)
+constexpr int ONE_WAVE_MAX_PODS = 16384;
 
 // Requests up to this size reserve with one fetch-and-subtract (undone on
 // failure) instead of a compare-and-swap loop: a herd of m pods picking one
@@ -173,21 +178,17 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         u64 bound;
         int r0, r1, r2;
     };
-    // branch-free fill: pods past p_end read a clamped, in-bounds row and are
-    // marked inactive (no usable key, complete list)
+    // branch-free fill: pods past p_end read a clamped, in-bounds row; they
+    // are `done` from the start of their window, so nothing reads their
+    // values -- no select on the loaded registers here, which would make the
+    // prefetch of the next window wait for its loads on the spot
     auto load = [&](int base, Pod &c) {
-        const int i = base + tid;
-        const bool ok = i < p_end;
-        const int ii = min(i, Pp - 1);
+        const int ii = min(base + tid, Pp - 1);
         load8(cand_key + (size_t)ii * KC, c.k);
-        const u64 b = cand_bound[ii];
-        const int r0 = req[ii], r1 = req[Pp + ii], r2 = req[2 * Pp + ii];
-#pragma unroll
-        for (int j = 0; j < KC; ++j) c.k[j] = ok ? c.k[j] : KEY_INVALID;
-        c.bound = ok ? b : KEY_INVALID;
-        c.r0 = r0;
-        c.r1 = r1;
-        c.r2 = r2;
+        c.bound = cand_bound[ii];
+        c.r0 = req[ii];
+        c.r1 = req[Pp + ii];
+        c.r2 = req[2 * Pp + ii];
     };
     auto publish = [&](int n, const Pod &c) {
         if (LDS_CAP || !pub || n < 0) return;
@@ -313,6 +314,219 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         for (int i = tid; i < 3 * N; i += THREADS) cap_g[i] = capl[i];
 }
 
+// ---------------------------------------------------------------------------
+// k_commit_w: the same walk in ONE wave (a window of 64 pods per round).
+// No barriers at all -- a wave's LDS operations execute in order, so every
+// step sees the previous one -- and the lowest bad pod is a ballot.  The
+// reservations of one wave instruction are applied one lane after another,
+// so within a window the first failing pod is (in practice) the first pod
+// whose request truly does not fit after the pods below it: herds of pods
+// wanting the same node no longer stop at a spurious failure of an early
+// member, as they do across the 16 waves of k_commit.  Correctness never
+// depends on that order (the argument of step 3 holds for any atomic order);
+// only the number of rounds does.
+// ---------------------------------------------------------------------------
+// The next window's lists are prefetched by inline-asm loads the compiler's
+// waitcnt pass does not track, retired by one vmcnt(0) tied to every
+// destination register just before the window starts: with compiler-visible
+// loads hipcc waits for the prefetch right where it is issued (the loop-carried
+// registers look pending), and every window pays a full load latency.
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+struct PodRaw {
+    v4u k0, k1, k2, k3;
+    u64 bound;
+    int r0, r1, r2;
+};
+__device__ __forceinline__ void prefetch_pod(const u64 *kp, const u64 *bp, const int *q0,
+                                             const int *q1, const int *q2, PodRaw &o) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(o.k0) : "v"(kp) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(o.k1) : "v"(kp) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(o.k2) : "v"(kp) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off offset:48" : "=v"(o.k3) : "v"(kp) : "memory");
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(o.bound) : "v"(bp) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "=v"(o.r0) : "v"(q0) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "=v"(o.r1) : "v"(q1) : "memory");
+    asm volatile("global_load_dword %0, %1, off" : "=v"(o.r2) : "v"(q2) : "memory");
+}
+__device__ __forceinline__ void retire_pod(PodRaw &o) {
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(o.k0), "+v"(o.k1), "+v"(o.k2), "+v"(o.k3), "+v"(o.bound), "+v"(o.r0),
+                   "+v"(o.r1), "+v"(o.r2)
+                 :
+                 : "memory");
+}
+
+template <bool LDS_CAP>
+__global__ void __launch_bounds__(64)
+k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
+           const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
+           int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
+           int *__restrict__ halt, int *__restrict__ pub) {
+    const int cb = blockIdx.x;
+    cand_key += (size_t)cb * Pp * KC;
+    cand_bound += (size_t)cb * Pp;
+    req += (size_t)cb * 3 * Pp;
+    cap_g += (size_t)cb * 3 * N;
+    out_node += (size_t)cb * Pp;
+    out_cost += (size_t)cb * Pp;
+    halt += cb * STATUS_INTS;
+    if (pub) pub += (size_t)cb * 3 * N;
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    int *capl = smem;
+    const int lane = threadIdx.x;
+    const int h = __hip_atomic_load(halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool resume = p_begin < 0;
+    if (resume) {
+        if (h < 0) return;
+        p_begin = h;
+    } else if (h >= 0) {
+        return;
+    }
+    if (LDS_CAP) {
+        for (int i0 = lane; i0 < 3 * N; i0 += 8 * 64) {
+            int v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * 64;
+                v[u] = i < 3 * N ? cap_g[i] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * 64;
+                if (i < 3 * N) capl[i] = v[u];
+            }
+        }
+    }
+    int *cap = LDS_CAP ? capl : cap_g;
+    struct Pod {
+        u64 k[KC];
+        u64 bound;
+        int r0, r1, r2;
+    };
+    auto load = [&](int base, Pod &c) {  // as k_commit's: pods past p_end are `done`
+        const int ii = min(base + lane, Pp - 1);
+        load8(cand_key + (size_t)ii * KC, c.k);
+        c.bound = cand_bound[ii];
+        c.r0 = req[ii];
+        c.r1 = req[Pp + ii];
+        c.r2 = req[2 * Pp + ii];
+    };
+    auto publish = [&](int n, const Pod &c) {
+        if (LDS_CAP || !pub || n < 0) return;
+        atomicSub(pub + n, c.r0);
+        atomicSub(pub + N + n, c.r1);
+        atomicSub(pub + 2 * N + n, c.r2);
+    };
+    auto ld = [&](int idx) -> int {
+        if (LDS_CAP) return cap[idx];
+        return __hip_atomic_load(cap + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    Pod cur;
+    PodRaw nxt;
+    load(p_begin, cur);
+    if (lane == 0 && h >= 0) {
+        halt[0] = -1;
+        if (resume) halt[1] += 1;
+    }
+    int round = 0;
+    int stop = p_end;
+    for (int base = p_begin; base < p_end; base += 64) {
+        if (base + 64 < p_end) {  // prefetch the next window (untracked loads)
+            const int ii = min(base + 64 + lane, Pp - 1);
+            prefetch_pod(cand_key + (size_t)ii * KC, cand_bound + ii, req + ii, req + Pp + ii,
+                         req + 2 * Pp + ii, nxt);
+        }
+        const int i = base + lane;
+        bool done = i >= p_end;
+        while (true) {
+            int choice = -1;
+            unsigned ccost = 0;
+            if (!done) {
+#pragma unroll
+                for (int j = 0; j < KC; ++j) {
+                    const u64 k = cur.k[j];
+                    if (k == KEY_INVALID || k > cur.bound) break;
+                    const int n = (int)(unsigned)k;
+                    const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
+                    if (cur.r0 <= a && cur.r1 <= b && cur.r2 <= c) {
+                        choice = n;
+                        ccost = (unsigned)(k >> 32);
+                        break;
+                    }
+                }
+            }
+            const bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
+            bool g0 = false, g1 = false, g2 = false;
+            if (choice >= 0)
+                reserve3<LDS_CAP>(cap + choice, cap + N + choice, cap + 2 * N + choice, cur.r0,
+                                  cur.r1, cur.r2, g0, g1, g2);
+            const bool bad = rescore || (choice >= 0 && !(g0 && g1 && g2));
+            const u64 bm = __ballot(bad);
+            ++round;
+            if (bm == 0) {  // no conflict: every pending pod of the window commits
+                if (!done) {
+                    out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
+                    out_cost[i] = ccost;
+                    publish(choice, cur);
+                }
+                break;
+            }
+            const int sl = (int)__builtin_ctzll(bm);
+            const int s = base + sl;
+            if (!done && lane >= sl && choice >= 0) {
+                if (g0) atomicAdd(cap + choice, cur.r0);
+                if (g1) atomicAdd(cap + N + choice, cur.r1);
+                if (g2) atomicAdd(cap + 2 * N + choice, cur.r2);
+            }
+            if (!done && lane < sl) {
+                out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
+                out_cost[i] = ccost;
+                publish(choice, cur);
+                done = true;
+            }
+            if (__builtin_amdgcn_readlane((int)rescore, sl)) {
+                stop = s;
+                break;
+            }
+            if (!LDS_CAP) __threadfence_block();  // the releases above before the re-check
+            if (lane == sl) {
+                // pod s against the capacity left by the pods below it
+                const int n = choice;
+                if (cur.r0 <= ld(n) && cur.r1 <= ld(N + n) && cur.r2 <= ld(2 * N + n)) {
+                    atomicSub(cap + n, cur.r0);
+                    atomicSub(cap + N + n, cur.r1);
+                    atomicSub(cap + 2 * N + n, cur.r2);
+                    out_node[i] = n;
+                    out_cost[i] = ccost;
+                    publish(n, cur);
+                    done = true;
+                }
+            }
+        }
+        if (stop < p_end) break;
+        if (base + 64 < p_end) {
+            retire_pod(nxt);
+            const v4u kk[4] = {nxt.k0, nxt.k1, nxt.k2, nxt.k3};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                cur.k[2 * j] = ((u64)kk[j].y << 32) | kk[j].x;
+                cur.k[2 * j + 1] = ((u64)kk[j].w << 32) | kk[j].z;
+            }
+            cur.bound = nxt.bound;
+            cur.r0 = nxt.r0;
+            cur.r1 = nxt.r1;
+            cur.r2 = nxt.r2;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no untracked load outlives the walk
+    if (lane == 0) {
+        if (stop < p_end) *halt = stop;
+        halt[2] += round;
+    }
+    if (LDS_CAP)
+        for (int i = lane; i < 3 * N; i += 64) cap_g[i] = capl[i];
+}
+
 }  // namespace
 
 bool commit_in_lds(int N) { return N <= LDS_CAP_MAX_NODES; }
@@ -325,6 +539,21 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
+    if (Pp <= ONE_WAVE_MAX_PODS) {
+        if (N <= LDS_CAP_MAX_NODES) {
+            const size_t lds = 3 * (size_t)N * 4;
+            static std::atomic<unsigned long long> attr{0};
+            hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit_w<true>),
+                                        LDS_DYN_MAX, attr);
+            if (e != hipSuccess) return e;
+            k_commit_w<true><<<batch, 64, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
+                                                     out_node, oc, halt, nullptr);
+        } else {
+            k_commit_w<false><<<batch, 64, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
+                                                    out_node, oc, halt, pub);
+        }
+        return hipGetLastError();
+    }
     if (N <= LDS_CAP_MAX_NODES) {
         const size_t lds = 3 * (size_t)N * 4;
         static std::atomic<unsigned long long> attr{0};

@@ -157,13 +157,18 @@ struct Top4 {
 // default: ~1% ahead of 1 on the bench, 3 of 3 pairs), 1 pinned MFMA/ds_read
 // interleave, 2 s_setprio(1) around each MFMA cluster, 3 iglp_opt(0),
 // 4 iglp_opt(1).
-template <int DT, int EPI = 0, int SCHED = COST_SCHED, int PIPE = COST_PIPE, int GM = COST_GM>
+// RMAP: a gathered rescore view -- view row q's traffic is WA row rowmap[q]
+// (read in place by the LDS-DMA source addresses; rows past the view's count
+// read its last row and are never merged)
+template <int DT, int EPI = 0, int SCHED = COST_SCHED, int PIPE = COST_PIPE, int GM = COST_GM,
+          bool RMAP = false>
 __global__ void __launch_bounds__(THREADS, 1)
 k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
             u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base,
             const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
-            Ovf ov) {
+            Ovf ov, const int *__restrict__ rowmap) {
+    static_assert(!RMAP || PIPE == 0, "the row map is wired into the LDS-DMA staging only");
     using M = Mma<DT>;
     using acc_t = typename M::acc_t;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -241,11 +246,18 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         const int c = sq ^ ((row >> 1) & 7);
         glds16(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
     };
+    int bpod[4];  // RMAP: the WA rows of this lane's four B pieces
+    if constexpr (RMAP) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            bpod[j] = rowmap[min(p0 + nt * BN + (j * 8 + w) * 8 + srow_in, dyn_hi - 1)];
+    }
     auto pieceB = [&](int buf, int k0, int j) {
         const int r0 = (j * 8 + w) * 8;
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
-        glds16(Bg + (size_t)row * Kb + k0 + c * 16, bbuf(buf) + r0 * BKB);
+        const unsigned char *src = RMAP ? WA + (size_t)bpod[j] * Kb : Bg + (size_t)row * Kb;
+        glds16(src + k0 + c * 16, bbuf(buf) + r0 * BKB);
     };
     auto stageA = [&](int buf, int k0) {
 #pragma unroll
@@ -834,7 +846,7 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
 #define NAS_INST(E, S, PP, G)                                                                      \
     template __global__ void k_cost_topk<NAS_DT_I8, E, S, PP, G>(                                  \
         const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
-        u64 *, int, const int *, int, const int *, Ovf);
+        u64 *, int, const int *, int, const int *, Ovf, const int *);
 NAS_INST(0, 0, 0, 4) NAS_INST(1, 0, 0, 4) NAS_INST(0, 5, 0, 4) NAS_INST(1, 5, 0, 4)
 NAS_INST(3, 5, 0, 4) NAS_INST(0, 1, 0, 4) NAS_INST(0, 5, 0, 8) NAS_INST(4, 0, 0, 4)
 NAS_INST(0, 1, 2, 4) NAS_INST(0, 1, 3, 4) NAS_INST(0, 0, 2, 4) NAS_INST(0, 0, 3, 4)
@@ -846,12 +858,13 @@ NAS_INST(0, 0, 0, 2) NAS_INST(0, 0, 0, 16)
 
 #endif
 
-template <int DT>
+template <int DT, bool RMAP>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,
                          int p0, int np, const uint64_t *mask, uint64_t *partial,
                          uint64_t *pbound, int node_base, const Dyn *dyn, int batch,
-                         const Ovf &ov) {
-    const void *fn = reinterpret_cast<const void *>(&k_cost_topk<DT>);
+                         const Ovf &ov, const int32_t *rowmap) {
+    const void *fn = reinterpret_cast<const void *>(
+        &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP>);
     const int lds = lds_bytes<COST_PIPE>();
     static std::atomic<unsigned long long> attr_set{0};
     hipError_t e = set_lds_once(fn, lds, attr_set);
@@ -865,8 +878,8 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const int *ds = dyn ? dyn->start : nullptr;
     const int dh = dyn ? dyn->hi : 0;
     const int *dhp = dyn ? dyn->hi_ptr : nullptr;
-    k_cost_topk<DT><<<dim3(n_mt * n_nt, batch), THREADS, lds, st>>>(
-        lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dh, dhp, ov);
+    k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP><<<dim3(n_mt * n_nt, batch), THREADS, lds, st>>>(
+        lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dh, dhp, ov, rowmap);
     return hipGetLastError();
 }
 
@@ -877,8 +890,14 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base, const Dyn *dyn,
-                            int batch, const Ovf *ovf) {
+                            int batch, const Ovf *ovf, const int32_t *rowmap) {
     const Ovf ov = ovf ? *ovf : Ovf{};
+    if (rowmap && (!dyn || batch != 1)) return hipErrorInvalidValue;
+#define NAS_COST_DISPATCH(DTV, KB, OVV)                                                            \
+    (rowmap ? launch_cost_t<DTV, true>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound,     \
+                                       node_base, dyn, batch, OVV, rowmap)                        \
+            : launch_cost_t<DTV, false>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound,    \
+                                        node_base, dyn, batch, OVV, nullptr))
     if (dyn) {  // tiles covering any window [s, s + win) clipped to hi: one extra for the offset
         p0 = 0;
         np = (int)round_up(dyn->win, BN) + BN;
@@ -888,17 +907,15 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
     if (Mp % BM || np % BN || (!dyn && p0 + np > Pp)) return hipErrorInvalidValue;
     if (dtype == NAS_DT_I8) {
         if (Kp % BKB) return hipErrorInvalidValue;
-        return launch_cost_t<NAS_DT_I8>(st, Lt, WA, Mp, Kp, Pp, p0, np, mask, partial, pbound,
-                                        node_base, dyn, batch, ov);
+        return NAS_COST_DISPATCH(NAS_DT_I8, Kp, ov);
     }
     if (dtype == NAS_DT_F32) {
         if ((4 * Kp) % BKB) return hipErrorInvalidValue;
-        return launch_cost_t<NAS_DT_F32>(st, Lt, WA, Mp, 4 * Kp, Pp, p0, np, mask, partial, pbound,
-                                         node_base, dyn, batch, Ovf{});
+        return NAS_COST_DISPATCH(NAS_DT_F32, 4 * Kp, Ovf{});
     }
     if ((2 * Kp) % BKB) return hipErrorInvalidValue;
-    return launch_cost_t<NAS_DT_BF16>(st, Lt, WA, Mp, 2 * Kp, Pp, p0, np, mask, partial, pbound,
-                                      node_base, dyn, batch, Ovf{});
+    return NAS_COST_DISPATCH(NAS_DT_BF16, 2 * Kp, Ovf{});
+#undef NAS_COST_DISPATCH
 }
 
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,

@@ -33,7 +33,9 @@ __global__ void __launch_bounds__(FIT_THREADS)
 k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
       const int *__restrict__ req, int Pp, int p0, int p_end, unsigned long long *__restrict__ mask,
       const int *__restrict__ dyn_start, int dyn_win, const int *__restrict__ dyn_hi_ptr,
-      int block_pods) {
+      int block_pods, const int *__restrict__ rowmap, int rs) {
+    // rowmap (gathered rescore view): row q's requests are pod rowmap[q]'s,
+    // in the main request array (row stride rs); the mask keeps view rows
     if (dyn_start) {  // window [*dyn_start, +dyn_win) read from device memory (rescore slots)
         const int s = dyn_start[blockIdx.z * STATUS_INTS];
         if (s < 0) return;
@@ -45,7 +47,7 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
     if (pb0 >= p_end) return;  // whole block (no barriers below)
     const int cb = blockIdx.z;  // cluster of a batched launch
     cap += (size_t)cb * 3 * N;
-    req += (size_t)cb * 3 * Pp;
+    req += (size_t)cb * 3 * rs;
     mask += (size_t)cb * n_chunks * Pp;
     const int lane = threadIdx.x & 63;
     const int c = (int)blockIdx.y * FIT_WAVES + (int)(threadIdx.x >> 6);
@@ -80,15 +82,17 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
     const int pend = min(p_end, pb0 + block_pods);
     // lane i holds pod pb + i's requests (one coalesced load per resource),
     // the next group's loaded while this one is decided
-    int q = min(pb0 + lane, Pp - 1);
-    int na = req[q], nb = req[Pp + q], nd = req[2 * (size_t)Pp + q];
+    // rows past the range are clamped to its last row (loaded, never stored)
+    auto row = [&](int r) { const int q = min(r, p_end - 1); return rowmap ? rowmap[q] : q; };
+    int q = row(pb0 + lane);
+    int na = req[q], nb = req[rs + q], nd = req[2 * (size_t)rs + q];
     for (int pb = pb0; pb < pend; pb += 64) {
         const int ra = na, rb = nb, rd = nd;
         if (pb + 64 < pend) {
-            q = min(pb + 64 + lane, Pp - 1);
+            q = row(pb + 64 + lane);
             na = req[q];
-            nb = req[Pp + q];
-            nd = req[2 * (size_t)Pp + q];
+            nb = req[rs + q];
+            nd = req[2 * (size_t)rs + q];
         }
         const bool in = pb + lane < pend;
         // 64 pods at once against the chunk's extremes: fits every valid node
@@ -120,8 +124,9 @@ k_fit(const int *cap, int N, int n0, int nloc, int n_chunks,
 
 hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nloc, int Mp,
                       const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask,
-                      const Dyn *dyn, int batch) {
+                      const Dyn *dyn, int batch, const int32_t *rowmap, int req_stride) {
     (void)P;
+    if (rowmap && batch != 1) return hipErrorInvalidValue;
     if (np <= 0) return hipSuccess;
     const int n_chunks = Mp / 64;
     // pods per block: up to 512, fewer when the launch is small, so a rescore
@@ -136,7 +141,8 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
                                         dyn ? dyn->hi : p0 + np,
                                         reinterpret_cast<unsigned long long *>(mask),
                                         dyn ? dyn->start : nullptr, dyn ? dyn->win : 0,
-                                        dyn ? dyn->hi_ptr : nullptr, block_pods);
+                                        dyn ? dyn->hi_ptr : nullptr, block_pods, rowmap,
+                                        rowmap ? req_stride : Pp);
     return hipGetLastError();
 }
 

@@ -79,6 +79,7 @@ namespace {
 constexpr int RESCORE_PODS = 1024;  // pods per device-side rescore slot (multiple of COST_BN)
 constexpr int GATHER_PODS = 4096;   // dry pods rescored per gathered slot (gathered_slot)
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
+constexpr int MAX_SPEC_SLOTS = 8;         // speculative slots at most (nas_place, slot_hint)
 // ... except the second check: a walk still halted after a full batch is
 // usually nearly done (C2: 5 slots), and an idle slot's ~8 launches cost about
 // what one more host round trip does, so the second batch is one slot (C2
@@ -427,11 +428,8 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
 // stops cost launches, not synchronisations.
 int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t *pub, int hi) {
     const int R = std::min(GATHER_PODS, ctx->Pp);
-    const size_t row = (size_t)ctx->Kp * esz(ctx->dtype);
     OK(nas::ensure(ctx, ctx->g_words, (size_t)nas::stale_words(ctx->Pp) * 8));
     OK(nas::ensure(ctx, ctx->g_idx, (size_t)R * 4));
-    OK(nas::ensure(ctx, ctx->g_WA, (size_t)R * row));
-    OK(nas::ensure(ctx, ctx->g_req, (size_t)3 * R * 4));
     OK(nas::ensure(ctx, ctx->g_key, (size_t)R * KC * 8));
     OK(nas::ensure(ctx, ctx->g_bound, (size_t)R * 8));
     int32_t *halt = ctx->status.as<int32_t>();
@@ -439,23 +437,21 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t
     int32_t *idx = ctx->g_idx.as<int32_t>();
     auto *gk = ctx->g_key.as<uint64_t>();
     auto *gb = ctx->g_bound.as<uint64_t>();
-    hipEvent_t e0 = tm.mark(st);
+    hipEvent_t e0 = tm.fine(st);
     HIPCK(nas::launch_stale_scan(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, ctx->cap.as<int32_t>(), ctx->N,
                                  -1, hi, ctx->g_words.as<uint64_t>(), R, idx, ctl, halt));
-    HIPCK(nas::launch_gather_pods(st, idx, ctl + 1, ctx->WA.p, row, ctx->req.as<int32_t>(),
-                                  ctx->Pp, R, ctx->g_WA.p, ctx->g_req.as<int32_t>()));
     nas::Dyn dyn{ctl, R, 0, ctl + 1};
     auto *mask = ctx->mask.as<uint64_t>();
-    hipEvent_t e1 = tm.mark(st);
+    hipEvent_t e1 = tm.fine(st);
     HIPCK(nas::launch_fit(st, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
-                          ctx->g_req.as<int32_t>(), R, R, 0, R, mask, &dyn));
-    hipEvent_t e2 = tm.mark(st);
+                          ctx->req.as<int32_t>(), R, R, 0, R, mask, &dyn, 1, idx, ctx->Pp));
+    hipEvent_t e2 = tm.fine(st);
     const nas::Ovf ov = make_ovf(ctx, idx, ctl + 1);  // view row r is pod idx[r]
-    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->g_WA.p, ctx->Mp, ctx->Kp, R, 0, 0,
+    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, R, 0, 0,
                                 mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                ctx->Nloc0, &dyn, 1, &ov));
-    hipEvent_t e3 = tm.mark(st);
+                                ctx->Nloc0, &dyn, 1, &ov, idx));
+    hipEvent_t e3 = tm.fine(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     // the last merge writes the fresh lists straight into the pods' own list
     // slots (idx); with an exchange, the local merge first fills the view
@@ -474,7 +470,7 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t
         HIPCK(nas::launch_merge(st, xk, xb, ctx->world, (int64_t)R * KC, R, 0, 0, 0, ck, cbnd, 0,
                                 &dyn, 0, 1, 0, idx));
     }
-    hipEvent_t e4 = tm.mark(st);
+    hipEvent_t e4 = tm.fine(st);
     HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), ctx->Pp, -1, hi, ctx->cap.as<int32_t>(),
                              ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
@@ -483,7 +479,7 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t
     tm.span(T_COST, e2, e3);
     tm.span(T_MERGE, e3, e4);
     tm.span(T_COMMIT, e0, e1);
-    tm.span(T_COMMIT, e4, tm.mark(st));
+    tm.span(T_COMMIT, e4, tm.fine(st));
     return NAS_OK;
 }
 
@@ -841,7 +837,7 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->gather[0], &ctx->gbound[0], &ctx->gather[1], &ctx->gbound[1],
                       &ctx->resc_key, &ctx->resc_bound, &ctx->gather_r, &ctx->gbound_r,
                       &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
-                      &ctx->g_words, &ctx->g_idx, &ctx->g_WA, &ctx->g_req, &ctx->g_key,
+                      &ctx->g_words, &ctx->g_idx, &ctx->g_key,
                       &ctx->g_bound, &ctx->g_gk, &ctx->g_gb, &ctx->status, &ctx->scratch,
                       &ctx->vote_part, &ctx->vote_gather, &ctx->xsend[0], &ctx->xsend[1],
                       &ctx->ovf_ptr, &ctx->ovf_m, &ctx->ovf_e, &ctx->Lr};
@@ -1576,9 +1572,6 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     const uint32_t *raw = reinterpret_cast<const uint32_t *>(stage + P);  // decoded in place
     struct Landed { int lo, hi; hipEvent_t ev; };
     std::vector<Landed> landed;
-    hipEvent_t ready = tm.mark(st);
-    HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
-    HIPCK(hipStreamWaitEvent(sc, ready, 0));
     // chunk bounds; every scoring launch is enqueued before any commit-stream
     // work, so the host's enqueue time of merges / commits / copies never
     // delays the next chunk's cost launch
@@ -1592,7 +1585,13 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // merge / commit / copies stay on the scoring stream, which saves the
     // cross-stream event hops (~15-20 us each) that dominate a small pass
     // (C1 extended 0.41 -> 0.385 ms per nas_place)
-    if (chunks.size() == 1 && !ctx->comm) sc = st;
+    const bool one_stream = chunks.size() == 1 && !ctx->comm;
+    if (one_stream) sc = st;
+    if (!one_stream) {
+        hipEvent_t ready = tm.mark(st);
+        HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
+        HIPCK(hipStreamWaitEvent(sc, ready, 0));
+    }
     std::vector<hipEvent_t> scored(chunks.size());
     // fit + cost only on the two scoring streams (a chunk's tail blocks overlap
     // the next chunk; a third scoring stream measured 5% slower at G = 1 and
@@ -1623,9 +1622,17 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
                                  (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, sc));
         landed.push_back({lo, hi, tm.mark(sc)});
     }
-    HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
-    HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
+    if (!one_stream) {
+        HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
+        HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
+    }
     if (ctx->comm) inject_stall(ctx, st);  // behind every collective of the pass
+    // speculative slots: as many as the previous pass of this shape needed
+    // (consecutive passes over similar clusters stop alike), enqueued before
+    // the first status round trip; a slot whose walk is not halted exits at
+    // once.  Not with a communicator: every rank must issue the same slots.
+    const int spec = (!ctx->comm && ctx->slot_hint_P == P && ctx->slot_hint_N == N) ? ctx->slot_hint : 0;
+    for (int r = 0; r < spec; ++r) OK(gathered_slot(ctx, tm, st, nullptr, nullptr, P));
     hipEvent_t t1 = nullptr;
     auto fetch = [&]() -> int {
         // halt[0..2]: halt word, slot resumes, commit rounds; ctl[2]: pods rescored
@@ -1663,6 +1670,13 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     }
     OK(wait_event(ctx, t1));  // t1 follows everything on st (the status copies)
     int checks = 0;
+    if (hs[0] < 0 && hs[1] > 0) {
+        // speculative slots finished a walk that had halted: the per-chunk
+        // copies behind the commits predate them -- fetch everything again
+        OK(fetch());
+        unsched = 0;
+        unpack(0, P);
+    }
     while (hs[0] >= 0) {
         // still halted after the pipeline: more gathered slots, checked in batches
         if (hs[0] >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
@@ -1685,6 +1699,9 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     ctx->timings.rescored_pods = hs[3];
     ctx->timings.unschedulable = unsched;
     ctx->timings.commit_rounds = hs[2];
+    ctx->slot_hint = std::min(hs[1], MAX_SPEC_SLOTS);
+    ctx->slot_hint_P = P;
+    ctx->slot_hint_N = N;
     ctx->scored = true;
     return NAS_OK;
 }

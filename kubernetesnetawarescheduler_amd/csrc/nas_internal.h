@@ -77,6 +77,9 @@ struct nas_ctx {
     nas::DevBuf snap[6];              // cpu, mem, bw (f64) ; rx, tx, disk (i64)  [S][ns]
     int32_t n_orders = 0;
     bool orders_per_pod = false;      // nas_upload_pod_orders: set p belongs to pod p
+    // gathered slots the previous nas_place of shape (P, N) needed: enqueued
+    // speculatively by the next pass of that shape
+    int32_t slot_hint = 0, slot_hint_P = -1, slot_hint_N = -1;
     int64_t ord_ns = 0;               // row stride of order arrays
     nas::DevBuf order1, pos1;         // [n_orders][ord_ns]
     nas::DevBuf order2, pos2;         // [n_orders][ord_ns + 2]  (n+1 keys)
@@ -113,7 +116,7 @@ struct nas_ctx {
     nas::DevBuf gather_r, gbound_r;        // rescore slot exchange [world][win][KC] / [world][win]
     nas::DevBuf out_node, out_cost_f, out_cost_i;  // [Pp]
     nas::DevBuf g_words, g_idx;            // gathered rescore: dry-pod ballots, indices + count
-    nas::DevBuf g_WA, g_req, g_key, g_bound;  // gathered rescore view [R][Kp] / [3][R] / lists
+    nas::DevBuf g_key, g_bound;  // gathered rescore view's lists (rows read in place, row map g_idx)
     nas::DevBuf g_gk, g_gb;                // gathered rescore exchange [world][R][KC] / [world][R]
     nas::DevBuf status;      // small device scratch for commit control
     nas::DevBuf host_status; // pinned
@@ -201,14 +204,19 @@ struct Dyn {
 constexpr int MERGE_SRC_WINDOW = 1;  // k_merge source lists indexed from the window start
 constexpr int MERGE_DST_WINDOW = 2;  // k_merge destination indexed from the window start
 
+// rowmap (gathered rescore view, batch 1): view row q is pod rowmap[q] -- its
+// requests (k_fit, main array with row stride req_stride) and traffic row
+// (k_cost_topk, main WA) are read in place, no gathered copy
 hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nloc, int Mp,
                       const int32_t *req, int P, int Pp, int p0, int np, uint64_t *mask,
-                      const Dyn *dyn = nullptr, int batch = 1);
+                      const Dyn *dyn = nullptr, int batch = 1, const int32_t *rowmap = nullptr,
+                      int req_stride = 0);
 
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base,
-                            const Dyn *dyn = nullptr, int batch = 1, const Ovf *ovf = nullptr);
+                            const Dyn *dyn = nullptr, int batch = 1, const Ovf *ovf = nullptr,
+                            const int32_t *rowmap = nullptr);
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,
@@ -231,9 +239,6 @@ hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t
                              const int32_t *req, int Pp, const int32_t *cap, int N, int p0, int P,
                              uint64_t *words, int R, int32_t *idx, int32_t *ctl,
                              const int32_t *p0_dev = nullptr);
-hipError_t launch_gather_pods(hipStream_t st, const int32_t *idx, const int32_t *count,
-                              const void *WA, size_t row_bytes, const int32_t *req, int Pp, int Rv,
-                              void *WA_v, int32_t *req_v);
 
 // start of a nas_place pass: status[0] = -1 (halt), status[1 .. 2*STATUS_INTS)
 // = 0; cap_snap[0, n) = cap[0, n) when cap_snap is non-null

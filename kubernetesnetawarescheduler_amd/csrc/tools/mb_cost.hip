@@ -80,8 +80,11 @@ int main(int argc, char **argv) {
     for (int r = 0; r < reps; ++r) {
         for (int v = 0; v < nv; ++v) {
             if (!strchr(vsel, v < 26 ? 'a' + v : 'A' + v - 26)) continue;
+            // k_cost_topk's trailing row map (none); the experiment kernels
+            // take one argument fewer and ignore it
             void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero,
-                            (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf};
+                            (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf,
+                            &nodyn};
             CK(hipEventRecord(a));
             const int thr = strncmp(vars[v].name, "v3", 2) ? THREADS : THREADS3;  // v3 and v3T
             CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(thr), args, vars[v].lds, 0));

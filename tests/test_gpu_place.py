@@ -111,6 +111,38 @@ def test_rescore_path_runs(engine):
     assert (engine.get_capacity() == wfree).all()
 
 
+def test_repeat_passes_with_speculative_slots(engine):
+    """A pass that needed gathered rescore slots makes the next pass of the
+    same shape enqueue that many slots before its first status round trip
+    (nas_place slot_hint).  Every pass -- first, speculative repeats, a
+    different shape, and a shape that needs no slot after one that did --
+    equals the sequential oracle."""
+    rng = np.random.default_rng(78)
+    P, N = 2000, 256
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=30, cap_scale=0.02)
+    WA[:, :8] = 127
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    upload(engine, WA, L, free, req, "i8")
+    for it in range(3):
+        engine.reset_capacity()
+        node, _, ci = engine.place()
+        assert engine.timings()["rescore_rounds"] > 0, it
+        assert node.tolist() == want.tolist() and ci.tolist() == wcost.tolist(), it
+        assert (engine.get_capacity() == wfree).all(), it
+    # the same shape with roomy capacity: the speculative slots find nothing halted
+    roomy = np.minimum(free.astype(np.int64) * 5000, 2**31 - 1).astype(np.int32)
+    upload(engine, WA, L, roomy, req, "i8")
+    node, _, ci = engine.place()
+    w2, c2, f2 = oracle.place(WA, L, req, roomy, "i8")
+    assert engine.timings()["rescore_rounds"] == 0
+    assert node.tolist() == w2.tolist() and ci.tolist() == c2.tolist()
+    assert (engine.get_capacity() == f2).all()
+    # tight again: the hint is now 0, the host loop finds the stops itself
+    upload(engine, WA, L, free, req, "i8")
+    node, _, ci = engine.place()
+    assert node.tolist() == want.tolist() and ci.tolist() == wcost.tolist()
+
+
 @pytest.mark.parametrize("P,N", [(300, 200), (1000, 700)])
 def test_place_bf16_integer_valued_exact(engine, P, N):
     rng = np.random.default_rng(P + 3 * N)
