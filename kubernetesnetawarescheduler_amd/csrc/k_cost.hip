@@ -48,8 +48,14 @@ constexpr int TILE_BYTES = BM * BKB;          // 32 KiB: one operand, one stage
 #ifndef COST_PIPE
 #define COST_PIPE 0
 #endif
+// XCD tile order: GM > 0 = node-group major (GM node tiles x every pod tile);
+// GM = -PG = pod-group major (PG pod tiles x every node tile).  Pod groups of
+// 4 (32 concurrent workgroups per XCD = 8 node tiles x 4 pod tiles) fetch
+// fewer traffic rows from HBM per window and more latency rows from the
+// Infinity Cache (Lt, 105 MB, fits it): 2.0-2.5% faster than GM = 4 in 4 of 4
+// interleaved repetitions (profiles/r02_mb_cost_order.log)
 #ifndef COST_GM
-#define COST_GM 4
+#define COST_GM (-4)
 #endif
 // PIPE 0: A and B double-buffered (128 KiB).  PIPE 1: A (latency rows, mostly
 // L2/MALL-resident) double-buffered, B (the 1 GB traffic stream, mostly HBM)
@@ -200,7 +206,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         nt = first_nt + r % pg;
     }
     const int cb = blockIdx.y;  // cluster of a batched launch
-    Lt += (size_t)cb * n_mt * BM * Kb;
+    Lt += (size_t)cb * n_mt * BM * Kb;  // (tile order above: speed only)
     WA += (size_t)cb * Pp * Kb;
     mask += (size_t)cb * (n_mt * BM / 64) * Pp;
     partial += (size_t)cb * n_mt * Pp * KC;
