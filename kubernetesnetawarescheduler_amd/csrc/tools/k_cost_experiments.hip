@@ -710,5 +710,311 @@ NAS_INST3(0, 4, 4) NAS_INST3(1, 4, 4) NAS_INST3(3, 4, 4) NAS_INST3(4, 4, 4) NAS_
 NAS_INST3T(0, 4, 4) NAS_INST3T(1, 4, 4)
 #undef NAS_INST3T
 #endif
+// ---------------------------------------------------------------------------
+// k_cost_wide (measured round 2, kept for the record): the same contraction with NI x 128 pods per workgroup tile
+// (NI = 3: 256 nodes x 384 pods).  Every staged byte then feeds 1.2x the MACs
+// of the 256 x 256 tile -- 17% fewer bytes through the L2 -> LDS fabric, which
+// is what bounds k_cost_topk -- at the price of the whole LDS
+// (two 80 KiB stages) and 192 accumulator registers per wave (8 waves as
+// 2 node halves x 4 pod quarters, each 128 nodes x 32*NI pods).  PIPE 0
+// staging, LDS-DMA with the source-side swizzle, double-buffered fragments;
+// the epilogue writes each pod tile's 8-list to LDS as soon as it is built
+// (the accumulators of that tile die there), then the node-half waves merge.
+// Result (profiles/r02_mb_cost_wide.log): the main loop alone 4% faster than
+// NI = 2 (8.3-8.4 vs 8.7 ms), not the 17% the byte count predicts, and the
+// 3-tile epilogue at the 256-VGPR limit spills (10.2-10.3 ms in all) -- so the
+// staging fabric is not bound by bytes alone; k_cost_topk stays at 256 x 256.
+// ---------------------------------------------------------------------------
+template <int DT, int EPI, bool RMAP, int NI>
+__global__ void __launch_bounds__(THREADS, 1)
+k_cost_wide(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
+            int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
+            u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base,
+            const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
+            Ovf ov, const int *__restrict__ rowmap) {
+    constexpr int BNW = 128 * NI;     // pods per tile
+    constexpr int WP = 32 * NI;       // pods per wave
+    constexpr int BPC = BNW / 64;     // B pieces per wave per stage
+    constexpr int SB = (BM + BNW) * BKB;
+    using M = Mma<DT>;
+    using acc_t = typename M::acc_t;
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+    const int nwg = n_mt * n_nt;
+    const int b = blockIdx.x;
+    const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+    int mt, nt;
+    {  // pod-group major, groups of 4 pod tiles (k_cost_topk's COST_GM = -4)
+        constexpr int PG = 4;
+        const int gsize = PG * n_mt;
+        const int g = v / gsize, r = v % gsize;
+        const int first_nt = g * PG;
+        const int pg = min(n_nt - first_nt, PG);
+        mt = r / pg;
+        nt = first_nt + r % pg;
+    }
+    const int cb = blockIdx.y;
+    Lt += (size_t)cb * n_mt * BM * Kb;
+    WA += (size_t)cb * Pp * Kb;
+    mask += (size_t)cb * (n_mt * BM / 64) * Pp;
+    partial += (size_t)cb * n_mt * Pp * KC;
+    pbound += (size_t)cb * n_mt * Pp;
+    if (dyn_start) {
+        const int s = dyn_start[cb * STATUS_INTS];
+        if (s < 0) return;
+        if (dyn_hi_ptr) dyn_hi = dyn_hi_ptr[cb * STATUS_INTS];
+        p0 = s / BNW * BNW;
+        if (p0 + nt * BNW >= dyn_hi) return;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w >> 2, wn = w & 3;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int pod0 = p0 + nt * BNW;  // first pod (view row) of the tile
+    const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
+    const unsigned char *Bg = WA + (size_t)pod0 * Kb;
+    const int srow_in = lane >> 3, sq = lane & 7;
+    int bpod[BPC];
+    if constexpr (RMAP) {
+#pragma unroll
+        for (int j = 0; j < BPC; ++j) bpod[j] = rowmap[min(pod0 + (j * 8 + w) * 8 + srow_in, dyn_hi - 1)];
+    }
+    auto stage = [&](int buf, int k0) {
+        unsigned char *base = lds + buf * SB;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r0 = (j * 8 + w) * 8, row = r0 + srow_in;
+            const int c = sq ^ ((row >> 1) & 7);
+            glds16(Ag + (size_t)row * Kb + k0 + c * 16, base + r0 * BKB);
+        }
+#pragma unroll
+        for (int j = 0; j < BPC; ++j) {
+            const int r0 = (j * 8 + w) * 8, row = r0 + srow_in;
+            const int c = sq ^ ((row >> 1) & 7);
+            const unsigned char *src = RMAP ? WA + (size_t)bpod[j] * Kb : Bg + (size_t)row * Kb;
+            glds16(src + k0 + c * 16, base + BM * BKB + r0 * BKB);
+        }
+    };
+    u64 mwp[NI][2];
+    if constexpr (EPI == 0) {
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+            for (int mi2 = 0; mi2 < 2; ++mi2) {
+                const int pod = pod0 + wn * WP + ni * 32 + fr;
+                const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
+                mwp[ni][mi2] = mask[(size_t)chunk * Pp + pod];
+            }
+    }
+    acc_t acc[4][NI];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = acc_t{};
+    if constexpr (DT == NAS_DT_I8 && EPI == 0) {
+        if (ov.ptr) {  // exact traffic beyond int8: see k_cost_topk
+            const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
+            const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) {
+                const int r = pod0 + wn * WP + ni * 32 + fr;
+                int beg = 0, end = 0;
+                if (r < cnt_lim) {
+                    const int pod = (ov.row_pod ? ov.row_pod[r] : r) + cb * Pp;
+                    beg = ov.ptr[pod];
+                    end = ov.ptr[pod + 1];
+                }
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+                    for (int j = beg; j < end; ++j) {
+                        const int e = ov.e[j];
+                        const signed char *row = lr + (size_t)ov.m[j] * (n_mt * BM) + mi * 32;
+#pragma unroll
+                        for (int g = 0; g < 4; ++g) {
+                            const int x = *reinterpret_cast<const int *>(row + 8 * g);
+#pragma unroll
+                            for (int c = 0; c < 4; ++c)
+                                acc[mi][ni][4 * g + c] += e * (int)(signed char)(x >> (8 * c));
+                        }
+                    }
+            }
+        }
+    }
+    auto compute = [&](int buf) {
+        const unsigned char *As = lds + buf * SB;
+        const unsigned char *Bs = As + BM * BKB;
+        v4i a[2][4], bb[2][NI];
+        auto read = [&](int kk, v4i (&ra)[4], v4i (&rb)[NI]) {
+            const int c = kk * 2 + fh;
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int r = wm * 128 + mi * 32 + fr;
+                ra[mi] = *reinterpret_cast<const v4i *>(As + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) {
+                const int r = wn * WP + ni * 32 + fr;
+                rb[ni] = *reinterpret_cast<const v4i *>(Bs + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+        };
+        read(0, a[0], bb[0]);
+#pragma unroll
+        for (int kk = 0; kk < BKB / 32; ++kk) {
+            if (kk + 1 < BKB / 32) read(kk + 1, a[(kk + 1) & 1], bb[(kk + 1) & 1]);
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < NI; ++ni)
+                    acc[mi][ni] = M::mma(a[kk & 1][mi], bb[kk & 1][ni], acc[mi][ni]);
+        }
+    };
+    const int nk = Kb / BKB;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nk; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < nk) stage(cur ^ 1, (t + 1) * BKB);
+        compute(cur);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if constexpr (EPI == 1) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                asm volatile("" ::"v"(acc[mi][ni]));
+#endif
+            }
+        return;
+    }
+    // ---- epilogue: per pod tile ni, the lane's top-4 -> lane^32 merge -> an
+    // 8-list + bound, straight to LDS (staging is dead after the last barrier):
+    // xk[wm][wn][ni][32][9]
+    u64 *xk = reinterpret_cast<u64 *>(lds);
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+        const u64 *mw = mwp[ni];
+        unsigned u[4][16];
+        unsigned kmin = 0xffffffffu, kmax = 0u;
+        int smin = 0x7fffffff, smax = -0x7fffffff - 1;
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                if constexpr (DT == NAS_DT_I8) {
+                    smin = min(smin, (int)acc[mi][ni][reg]);
+                    smax = max(smax, (int)acc[mi][ni][reg]);
+                } else {
+                    u[mi][reg] = M::okey(acc[mi][ni][reg]);
+                    kmin = min(kmin, u[mi][reg]);
+                    kmax = max(kmax, u[mi][reg]);
+                }
+            }
+        if constexpr (DT == NAS_DT_I8) {
+            kmin = M::okey(smin);
+            kmax = M::okey(smax);
+        }
+        u64 k4[4];
+        if (__all(kmax - kmin < (1u << 26) - 1u)) {
+            unsigned c0 = 0xffffffffu, c1 = c0, c2 = c0, c3 = c0;
+            const unsigned nk6 = 0u - ((DT == NAS_DT_I8 ? (unsigned)smin : kmin) << 6);
+#pragma unroll
+            for (int mi2 = 0; mi2 < 2; ++mi2)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int mi = mi2 * 2 + h;
+                    const unsigned nbits = ~(unsigned)(mw[mi2] >> (32 * h));
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg) {
+                        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
+                        const unsigned raw = DT == NAS_DT_I8 ? (unsigned)(int)acc[mi][ni][reg]
+                                                             : u[mi][reg];
+                        const unsigned x = ((raw << 6) + nk6) | (unsigned)(mi * 16 + reg) |
+                                           (unsigned)__builtin_amdgcn_sbfe((int)nbits, row, 1);
+                        c3 = umed3(c2, c3, x);
+                        c2 = umed3(c1, c2, x);
+                        c1 = umed3(c0, c1, x);
+                        c0 = min(c0, x);
+                    }
+                }
+            const unsigned cc[4] = {c0, c1, c2, c3};
+            const unsigned nb = (unsigned)(node_base + mt * BM + wm * 128 + 4 * fh);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const unsigned i = cc[j] & 63u, r = i & 15u;
+                const unsigned node = nb + (i >> 4) * 32u + (r & 3u) + 8u * (r >> 2);
+                k4[j] = cc[j] == 0xffffffffu ? KEY_INVALID
+                                             : ((u64)((cc[j] >> 6) + kmin) << 32) | node;
+            }
+        } else {
+            Top4 t4;
+            t4.init();
+#pragma unroll
+            for (int mi2 = 0; mi2 < 2; ++mi2)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int mi = mi2 * 2 + h;
+                    const unsigned bits = (unsigned)(mw[mi2] >> (32 * h));
+                    const unsigned node0 = (unsigned)(node_base + mt * BM + wm * 128 + mi * 32);
+#pragma unroll
+                    for (int reg = 0; reg < 16; ++reg) {
+                        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
+                        const unsigned key = DT == NAS_DT_I8 ? M::okey(acc[mi][ni][reg]) : u[mi][reg];
+                        const unsigned x = key | ((((bits >> row) & 1u) ^ 1u) * 0xffffffffu);
+                        t4.insert(x, node0 + row);
+                    }
+                }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) k4[j] = t4.c[j] == 0xffffffffu ? KEY_INVALID : t4.key(j);
+        }
+        u64 o4[4], l8[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o4[j] = shfl_xor64(k4[j], 32);
+        merge44(k4, o4, l8);
+        if (fh == 0) {
+            u64 *d = xk + (((wm * 4 + wn) * NI + ni) * 32 + fr) * 9;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = l8[j];
+            d[8] = umin64(k4[3], o4[3]);
+        }
+    }
+    __syncthreads();
+    // the node-half waves' lists of each pod merged: waves wm = 0 take the
+    // 4 * WP pods, lane l pods l and l + 64 (when < WP)
+    if (wm == 0) {
+#pragma unroll
+        for (int q = 0; q < (WP + 63) / 64; ++q) {
+            const int pp = q * 64 + lane;  // pod within the wave's WP pods
+            if (pp < WP) {
+                const int ni = pp >> 5, f = pp & 31;
+                const u64 *s0 = xk + (((0 * 4 + wn) * NI + ni) * 32 + f) * 9;
+                const u64 *s1 = xk + (((1 * 4 + wn) * NI + ni) * 32 + f) * 9;
+                u64 mine[8], other[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    mine[j] = s0[j];
+                    other[j] = s1[j];
+                }
+                merge88(mine, other);
+                const u64 bd = umin64(umin64(s0[8], s1[8]), mine[7]);
+                const int pod = pod0 + wn * WP + pp;
+                store8(partial + ((size_t)mt * Pp + pod) * KC, mine);
+                pbound[(size_t)mt * Pp + pod] = bd;
+            }
+        }
+    }
+}
+
+#ifdef NAS_DIAG_VARIANTS
+#define NAS_INSTW(E, NI)                                                                           \
+    template __global__ void k_cost_wide<NAS_DT_I8, E, false, NI>(                                 \
+        const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
+        u64 *, int, const int *, int, const int *, Ovf, const int *);
+NAS_INSTW(0, 2) NAS_INSTW(1, 2) NAS_INSTW(0, 3) NAS_INSTW(1, 3)
+#undef NAS_INSTW
+#endif
 }  // namespace
 }  // namespace nas

@@ -19,7 +19,7 @@ int main(int argc, char **argv) {
     const int P = argc > 2 ? atoi(argv[2]) : 100000;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
     const char *vsel = argc > 4 ? argv[4] : "abcdefgh";  // variants to run (a..)
-    const int Mp = (int)round_up(N, 256), Kp = (int)round_up(N, 256), Pp = (int)round_up(P, 256);
+    const int Mp = (int)round_up(N, 256), Kp = (int)round_up(N, 256), Pp = (int)round_up(P, 768);
     void *Lt, *WA, *mask, *partial, *pbound;
     CK(hipMalloc(&Lt, (size_t)Mp * Kp));
     CK(hipMalloc(&WA, (size_t)Pp * Kp));
@@ -62,7 +62,10 @@ int main(int argc, char **argv) {
 #define KV3T(E, S, G) (const void *)&k_cost_topk3<NAS_DT_I8, E, S, G, true>, (S) * TILE_BYTES
                       {"v2T/top4/st4", KV2T(0, 4, 4)}, {"v2T/noepi/st4", KV2T(1, 4, 4)},
                       {"v2T/top4/st3", KV2T(0, 3, 4)}, {"v3T/top4", KV3T(0, 4, 4)},
-                      {"v3T/noepi", KV3T(1, 4, 4)}};
+                      {"v3T/noepi", KV3T(1, 4, 4)},
+#define KVW(E, NI) (const void *)&k_cost_wide<NAS_DT_I8, E, false, NI>, 2 * (BM + 128 * NI) * BKB
+                      {"wide2/top4", KVW(0, 2)}, {"wide2/noepi", KVW(1, 2)},
+                      {"wide3/top4", KVW(0, 3)}, {"wide3/noepi", KVW(1, 3)}};
     const int nv = sizeof(vars) / sizeof(vars[0]);
     for (int v = 0; v < nv; ++v)
         CK(hipFuncSetAttribute(vars[v].fn, hipFuncAttributeMaxDynamicSharedMemorySize, vars[v].lds));
@@ -87,7 +90,12 @@ int main(int argc, char **argv) {
                             &nodyn};
             CK(hipEventRecord(a));
             const int thr = strncmp(vars[v].name, "v3", 2) ? THREADS : THREADS3;  // v3 and v3T
-            CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * n_nt), dim3(thr), args, vars[v].lds, 0));
+            // wide3: 384-pod tiles (Pp rounded to 768 below, so both divide)
+            const int nnt = strncmp(vars[v].name, "wide3", 5) ? n_nt : Pp / 384;
+            void *argw[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&nnt, &zero,
+                            (void *)&Pp, &mk, &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf,
+                            &nodyn};
+            CK(hipLaunchKernel(vars[v].fn, dim3(n_mt * nnt), dim3(thr), strncmp(vars[v].name, "wide3", 5) ? args : argw, vars[v].lds, 0));
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms;
