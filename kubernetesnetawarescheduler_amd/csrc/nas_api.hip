@@ -1633,6 +1633,14 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // once.  Not with a communicator: every rank must issue the same slots.
     const int spec = (!ctx->comm && ctx->slot_hint_P == P && ctx->slot_hint_N == N) ? ctx->slot_hint : 0;
     for (int r = 0; r < spec; ++r) OK(gathered_slot(ctx, tm, st, nullptr, nullptr, P));
+    if (spec > 0) {
+        // behind the slots, all placements again: when they finished the walk,
+        // the status round trip below brings the final results with it
+        HIPCK(hipMemcpyAsync(stage, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+        if (want_raw)
+            HIPCK(hipMemcpyAsync(stage + P, ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost,
+                                 st));
+    }
     hipEvent_t t1 = nullptr;
     auto fetch = [&]() -> int {
         // halt[0..2]: halt word, slot resumes, commit rounds; ctl[2]: pods rescored
@@ -1670,10 +1678,10 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     }
     OK(wait_event(ctx, t1));  // t1 follows everything on st (the status copies)
     int checks = 0;
-    if (hs[0] < 0 && hs[1] > 0) {
+    if (spec > 0 && hs[0] < 0 && hs[1] > 0) {
         // speculative slots finished a walk that had halted: the per-chunk
-        // copies behind the commits predate them -- fetch everything again
-        OK(fetch());
+        // copies behind the commits predate them; the full copy behind the
+        // slots (same round trip) holds the final placements
         unsched = 0;
         unpack(0, P);
     }

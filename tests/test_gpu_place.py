@@ -299,14 +299,17 @@ def test_rescore_slots_across_chunks(engine):
     assert (engine.get_capacity() == wfree).all()
 
 
-def test_l2_commit_published_capacity(engine):
-    """More nodes than the LDS commit holds (N > 13653): the commit works on
+@pytest.mark.parametrize("P", [20000, 6000])
+def test_l2_commit_published_capacity(engine, P):
+    """More nodes than the LDS commit holds (N > 13,610): the commit works on
     the capacity in L2 with speculative reservations, and the pipelined
     scoring chunks read the published capacity it maintains (start minus
     committed pods).  Crowded preferences and 2 pod slots per node make many
-    lists run dry; every placement must still equal the sequential oracle."""
+    lists run dry; every placement must still equal the sequential oracle.
+    P = 20000 walks in 1024-pod windows (k_commit), P = 6000 in one wave
+    (k_commit_w, walks of up to 16,384 pods)."""
     rng = np.random.default_rng(31)
-    P, N = 20000, 14000
+    N = 14000
     L = rng.integers(1, 100, (N, N)).astype(np.int8)
     a = rng.integers(0, 64, P)
     b = (a + 1 + rng.integers(0, 63, P)) % 64
