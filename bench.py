@@ -85,7 +85,10 @@ def cpu_info():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count()
-    return {"model": model, "nproc": os.cpu_count(), "usable": usable}
+    # the box's CPU share: OMP_NUM_THREADS (16 on the GPU pool; `nproc` reports
+    # it too), while affinity and os.cpu_count() show the whole machine
+    return {"model": model, "nproc": os.cpu_count(), "usable": usable,
+            "omp_num_threads": int(os.environ.get("OMP_NUM_THREADS", "0")) or None}
 
 
 def pmc_traffic(args):
