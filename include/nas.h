@@ -55,9 +55,11 @@ extern "C" {
 #define NAS_DT_BF16 2 /* bf16 bits (uint16), fp32 accumulation */
 #define NAS_DT_I32 3  /* traffic only, with NAS_DT_I8 latency: int32 traffic, exact integer
                        * scores (see nas_upload_traffic_dense) */
-#define NAS_DT_F32 4  /* fp32 latency and traffic as measured (no quantisation): exact
-                       * fp32 products on v_mfma_f32_32x32x2_f32, fp32 accumulation --
-                       * costs within 1e-5 relative of an fp64 sum */
+#define NAS_DT_F32 4  /* fp32 latency and traffic as measured (no quantisation): each
+                       * operand split into three bf16 planes (x = h + m + l), the
+                       * products to 2^-24 relative on the bf16 MFMA (six terms),
+                       * fp32 accumulation -- costs within 1e-5 relative of an fp64
+                       * sum */
 
 /* winner slots returned by nas_score_reference (order of scheduler.go:360-365) */
 #define NAS_W_CPU 0

@@ -11,7 +11,9 @@
 //
 //  * int8 path: v_mfma_i32_32x32x32_i8, int32 accumulation -- exact, so the
 //    integer scores and the chosen nodes are bit-identical to the oracle.
-//  * bf16 path: v_mfma_f32_32x32x16_bf16, fp32 accumulation.
+//  * bf16 path: v_mfma_f32_32x32x16_bf16, fp32 accumulation; also the fp32
+//    path, whose operands are split into three bf16 planes each and laid out
+//    along a six-fold K (k_misc.hip k_split6: products to 2^-24 relative).
 //
 // Tile: 256 nodes x 256 pods per 512-thread workgroup (8 wave64 as 2 x 4),
 // each wave 128 nodes x 64 pods = 4 x 2 MFMA 32x32 tiles.  K is staged 128
@@ -84,27 +86,6 @@ struct Mma<NAS_DT_I8> {
         return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
     }
     static __device__ __forceinline__ unsigned okey(int x) { return (unsigned)x ^ 0x80000000u; }
-};
-
-// fp32: one 16-byte fragment holds 4 k-values per lane; element j of lane
-// half h is k-pair j of the MFMA (any permutation of K works when A and B use
-// the same one), so a fragment pair is 4 v_mfma_f32_32x32x2_f32 -- exact fp32
-// products, fp32 accumulation
-template <>
-struct Mma<NAS_DT_F32> {
-    using acc_t = v16f;
-    static __device__ __forceinline__ acc_t mma(v4i a, v4i b, acc_t c) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            c = __builtin_amdgcn_mfma_f32_32x32x2f32(__int_as_float(a[j]), __int_as_float(b[j]), c,
-                                                     0, 0, 0);
-        return c;
-    }
-    static __device__ __forceinline__ unsigned okey(float x) {
-        x = x + 0.0f;
-        const unsigned u = __float_as_uint(x);
-        return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-    }
 };
 
 template <>
@@ -915,10 +896,9 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
         if (Kp % BKB) return hipErrorInvalidValue;
         return NAS_COST_DISPATCH(NAS_DT_I8, Kp, ov);
     }
-    if (dtype == NAS_DT_F32) {
-        if ((4 * Kp) % BKB) return hipErrorInvalidValue;
-        return NAS_COST_DISPATCH(NAS_DT_F32, 4 * Kp, Ovf{});
-    }
+    // (NAS_DT_F32 operands arrive here as their bf16 six-segment splits,
+    // dtype NAS_DT_BF16: nas_api.hip launch_cost)
+    if (dtype != NAS_DT_BF16) return hipErrorInvalidValue;
     if ((2 * Kp) % BKB) return hipErrorInvalidValue;
     return NAS_COST_DISPATCH(NAS_DT_BF16, 2 * Kp, Ovf{});
 #undef NAS_COST_DISPATCH

@@ -378,6 +378,45 @@ __global__ void k_rehearse_replicate(unsigned long long *__restrict__ a, long lo
     }
 }
 
+// fp32 -> bf16, round to nearest even (finite inputs)
+__device__ __forceinline__ unsigned short bf16_rne(float x) {
+    const unsigned u = __float_as_uint(x);
+    return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+
+// The fp32 contraction as a bf16 one (nas_api.hip prepare_split): x = h + m +
+// l with h = bf16(x), m = bf16(x - h), l = bf16(x - h - m) (each residual is
+// exact in fp32), and the K axis extended six-fold so that sum_k A'[k] B'[k]
+// = sum_k (Ah Bh + Ah Bm + Am Bh + Ah Bl + Al Bh + Am Bm): every term of the
+// exact product down to 2^-24 relative; the dropped Am Bl + Al Bm + Al Bl are
+// below 2^-23 of it.  Products of bf16 pairs are exact in the MFMA's fp32
+// accumulation.  Segment s of a row holds plane A_PAT[s] (latency, pattern
+// 0) or B_PAT[s] (traffic, pattern 1) of that row's K values.
+__global__ void k_split6(const float *__restrict__ src, unsigned short *__restrict__ dst,
+                         long long rows, int Kp, int pattern) {
+    const long long n = rows * Kp;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n;
+         t += (long long)gridDim.x * blockDim.x) {
+        const long long r = t / Kp;
+        const int k = (int)(t - r * Kp);
+        const float x = src[t];
+        const unsigned short h = bf16_rne(x);
+        const float r1 = x - bf16_f(h);
+        const unsigned short m = bf16_rne(r1);
+        const unsigned short l = bf16_rne(r1 - bf16_f(m));
+        // A: h h m h l m     B: h m h l h m
+        unsigned short *d = dst + (size_t)r * 6 * Kp + k;
+        if (pattern == 0) {
+            d[0] = h; d[(size_t)Kp] = h; d[(size_t)2 * Kp] = m;
+            d[(size_t)3 * Kp] = h; d[(size_t)4 * Kp] = l; d[(size_t)5 * Kp] = m;
+        } else {
+            d[0] = h; d[(size_t)Kp] = m; d[(size_t)2 * Kp] = h;
+            d[(size_t)3 * Kp] = l; d[(size_t)4 * Kp] = h; d[(size_t)5 * Kp] = m;
+        }
+    }
+}
+
 }  // namespace
 
 hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
@@ -427,6 +466,15 @@ hipError_t launch_scatter_f32(hipStream_t st, const int32_t *pod, const int32_t 
                               const float *val, int64_t n, int Kp, float *WA) {
     if (n <= 0) return hipSuccess;
     k_scatter_f32<<<grid_for(n, 256), 256, 0, st>>>(pod, node, val, (long long)n, Kp, WA);
+    return hipGetLastError();
+}
+
+hipError_t launch_split6(hipStream_t st, const float *src, uint16_t *dst, int64_t rows, int Kp,
+                         int pattern) {
+    if (rows <= 0) return hipSuccess;
+    const long long n = rows * (long long)Kp;
+    k_split6<<<(int)std::min<long long>((n + 255) / 256, 65536), 256, 0, st>>>(
+        src, reinterpret_cast<unsigned short *>(dst), (long long)rows, Kp, pattern);
     return hipGetLastError();
 }
 

@@ -278,6 +278,36 @@ int prepare_ovf(nas_ctx *ctx) {
     return NAS_OK;
 }
 
+// NAS_DT_F32 scores on the bf16 MFMA: both operands split into six K-segments
+// of bf16 planes (k_misc.hip k_split6), once per upload; every cost launch
+// then runs the bf16 kernel over K' = 6 Kp (launch_cost below)
+int prepare_split(nas_ctx *ctx) {
+    if (ctx->dtype != NAS_DT_F32 || ctx->split_valid) return NAS_OK;
+    const int64_t lrows = (int64_t)ctx->B * ctx->Mp, wrows = (int64_t)ctx->B * ctx->Pp;
+    OK(nas::ensure(ctx, ctx->Lt6, (size_t)lrows * 6 * ctx->Kp * 2));
+    OK(nas::ensure(ctx, ctx->WA6, (size_t)wrows * 6 * ctx->Kp * 2));
+    HIPCK(nas::launch_split6(ctx->stream, ctx->Lt.as<float>(), ctx->Lt6.as<uint16_t>(), lrows,
+                             ctx->Kp, 0));
+    HIPCK(nas::launch_split6(ctx->stream, ctx->WA.as<float>(), ctx->WA6.as<uint16_t>(), wrows,
+                             ctx->Kp, 1));
+    ctx->split_valid = true;
+    return NAS_OK;
+}
+
+// one cost/top-k launch over the main traffic rows (or a row-mapped view)
+hipError_t launch_cost(nas_ctx *ctx, hipStream_t st, int Pp, int p0, int np, const uint64_t *mask,
+                       const nas::Dyn *dyn, int batch, const nas::Ovf *ov,
+                       const int32_t *rowmap = nullptr) {
+    if (ctx->dtype == NAS_DT_F32)
+        return nas::launch_cost_topk(st, NAS_DT_BF16, ctx->Lt6.p, ctx->WA6.p, ctx->Mp, 6 * ctx->Kp,
+                                     Pp, p0, np, mask, ctx->partial.as<uint64_t>(),
+                                     ctx->pbound.as<uint64_t>(), ctx->Nloc0, dyn, batch, nullptr,
+                                     rowmap);
+    return nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, Pp, p0, np,
+                                 mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
+                                 ctx->Nloc0, dyn, batch, ov, rowmap);
+}
+
 // exact traffic row (n values, each within int32) -> the int8 plane row and
 // the row's overflow entries (node, excess)
 void split_row(const int64_t *v, int n, signed char *plane, std::vector<int32_t> &m,
@@ -406,9 +436,7 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
                           p_hi - p_lo, mask));
     hipEvent_t e1 = tm.fine(st);
     const nas::Ovf ov = make_ovf(ctx);
-    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, v.WA, ctx->Mp, ctx->Kp, v.Pp, pr0, np,
-                                mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                ctx->Nloc0, nullptr, 1, &ov));
+    HIPCK(launch_cost(ctx, st, v.Pp, pr0, np, mask, nullptr, 1, &ov));
     hipEvent_t e2 = tm.fine(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
@@ -448,9 +476,7 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t
                           ctx->req.as<int32_t>(), R, R, 0, R, mask, &dyn, 1, idx, ctx->Pp));
     hipEvent_t e2 = tm.fine(st);
     const nas::Ovf ov = make_ovf(ctx, idx, ctl + 1);  // view row r is pod idx[r]
-    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, R, 0, 0,
-                                mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                ctx->Nloc0, &dyn, 1, &ov, idx));
+    HIPCK(launch_cost(ctx, st, R, 0, 0, mask, &dyn, 1, &ov, idx));
     hipEvent_t e3 = tm.fine(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     // the last merge writes the fresh lists straight into the pods' own list
@@ -506,9 +532,7 @@ int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi, int32_t *pub = nullptr) {
     HIPCK(nas::launch_fit(sc, ctx->cap.as<int32_t>(), ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp,
                           ctx->req.as<int32_t>(), ctx->P, ctx->Pp, 0, RESCORE_PODS, mask, &dyn, B));
     const nas::Ovf ov = make_ovf(ctx);
-    HIPCK(nas::launch_cost_topk(sc, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, ctx->Pp, 0,
-                                0, mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                ctx->Nloc0, &dyn, B, &ov));
+    HIPCK(launch_cost(ctx, sc, ctx->Pp, 0, 0, mask, &dyn, B, &ov));
     const int n_lists = ctx->Mp / nas::COST_BM;
     if (!exchanging(ctx)) {
         HIPCK(nas::launch_merge(sc, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
@@ -546,9 +570,7 @@ int score_batch(nas_ctx *ctx, Timer &tm) {
                           Pp, 0, P, mask, nullptr, B));
     hipEvent_t e1 = tm.mark(st);
     const nas::Ovf ov = make_ovf(ctx);
-    HIPCK(nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, Pp, 0, Pp,
-                                mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), 0,
-                                nullptr, B, &ov));
+    HIPCK(launch_cost(ctx, st, Pp, 0, Pp, mask, nullptr, B, &ov));
     hipEvent_t e2 = tm.mark(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
@@ -840,7 +862,7 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->g_words, &ctx->g_idx, &ctx->g_key,
                       &ctx->g_bound, &ctx->g_gk, &ctx->g_gb, &ctx->status, &ctx->scratch,
                       &ctx->vote_part, &ctx->vote_gather, &ctx->xsend[0], &ctx->xsend[1],
-                      &ctx->ovf_ptr, &ctx->ovf_m, &ctx->ovf_e, &ctx->Lr};
+                      &ctx->ovf_ptr, &ctx->ovf_m, &ctx->ovf_e, &ctx->Lr, &ctx->Lt6, &ctx->WA6};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
@@ -1177,6 +1199,7 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
     ctx->L_dtype = dtype;
     ctx->synth_valid = false;
     ctx->lr_valid = false;
+    ctx->split_valid = false;
     ctx->scored = false;
     return NAS_OK;
 }
@@ -1278,6 +1301,7 @@ static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
     ctx->wa_dtype = dtype;
     ctx->ovf_n = 0;
     ctx->wa_abs_row_max = 0;
+    ctx->split_valid = false;
     ctx->scored = false;  // the lists (and their buffers' sizes) belong to the old inputs
     ctx->have_wa = false;
     return NAS_OK;
@@ -1520,6 +1544,7 @@ int nas_score(nas_ctx *ctx) {
     OK(check_extended(ctx));
     OK(alloc_extended(ctx));
     OK(prepare_ovf(ctx));
+    OK(prepare_split(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     if (ctx->B > 1) OK(score_batch(ctx, tm));
@@ -1543,6 +1568,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     if (!node_out) return nas::fail(ctx, NAS_ERR_ARG, "node_out null");
     OK(alloc_extended(ctx));
     OK(prepare_ovf(ctx));
+    OK(prepare_split(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     if (ctx->B > 1) return place_batch(ctx, tm, node_out, cost_out, int_score_out);
@@ -1756,6 +1782,7 @@ int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi) {
         return nas::fail(ctx, NAS_ERR_ARG, "nas_score_range: pod range");
     OK(alloc_extended(ctx));
     OK(prepare_ovf(ctx));
+    OK(prepare_split(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     OK(score_range(ctx, tm, p_lo, p_hi));
@@ -2046,6 +2073,7 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
     HIPCK(hipStreamSynchronize(ctx->stream));
     ctx->ovf_n = 0;
     ctx->lr_valid = false;
+    ctx->split_valid = false;
     ctx->scored = false;
     if (dtype == NAS_DT_I8) {
         // exact traffic: peer aggregates beyond the int8 plane go to the

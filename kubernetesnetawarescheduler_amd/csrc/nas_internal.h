@@ -80,6 +80,10 @@ struct nas_ctx {
     // gathered slots the previous nas_place of shape (P, N) needed: enqueued
     // speculatively by the next pass of that shape
     int32_t slot_hint = 0, slot_hint_P = -1, slot_hint_N = -1;
+    // NAS_DT_F32: the operands as six-segment bf16 splits (prepare_split);
+    // the fp32 Lt / WA stay for read-back and host-side updates
+    nas::DevBuf Lt6, WA6;
+    bool split_valid = false;
     int64_t ord_ns = 0;               // row stride of order arrays
     nas::DevBuf order1, pos1;         // [n_orders][ord_ns]
     nas::DevBuf order2, pos2;         // [n_orders][ord_ns + 2]  (n+1 keys)
@@ -254,6 +258,10 @@ hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int 
 hipError_t launch_csr_aggregate_bf16(hipStream_t st, const int32_t *row_ptr, const int32_t *peer,
                                      const uint16_t *w, int P, int N, int Kp, uint16_t *WA);
 // fp32 rows WA[p][m] = v for host-aggregated (pod, node, value) triples
+// fp32 operand -> six bf16 K-segments (pattern 0: latency h h m h l m,
+// 1: traffic h m h l h m), rows of 6 * Kp elements (k_misc.hip k_split6)
+hipError_t launch_split6(hipStream_t st, const float *src, uint16_t *dst, int64_t rows, int Kp,
+                         int pattern);
 hipError_t launch_scatter_f32(hipStream_t st, const int32_t *pod, const int32_t *node,
                               const float *val, int64_t n, int Kp, float *WA);
 // int8 plane entries WA[p][m] = v for host-aggregated (pod, node, value) triples

@@ -1,6 +1,7 @@
 """The fp32 network-cost path (include/nas.h NAS_DT_F32): measured, unquantised
-latency (microseconds) and traffic (MB) as fp32, exact fp32 products on
-v_mfma_f32_32x32x2_f32 with fp32 accumulation.  The north star's bar for raw
+latency (microseconds) and traffic (MB) as fp32; each operand split into three
+bf16 planes and contracted on the bf16 MFMA over a six-fold K (products to
+2^-24 relative) with fp32 accumulation.  The north star's bar for raw
 floating-point costs is 1e-5 relative to an fp64 sum (REL_TOL below); the
 chosen nodes must equal the fp64 sequential oracle's wherever the cost gap at
 a pod's turn exceeds that tolerance."""
