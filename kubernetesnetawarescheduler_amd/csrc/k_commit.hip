@@ -44,7 +44,7 @@ namespace {
 
 constexpr int THREADS = 1024;  // one window of pods per round
 constexpr int LDS_DYN_MAX = 160 * 1024 - 512;  // leaves room for the static LDS
-constexpr int LDS_CAP_MAX_NODES = LDS_DYN_MAX / 12;
+constexpr int LDS_CAP_MAX_NODES = (LDS_DYN_MAX - 256) / 12;  // + cap_to_lds padding
 constexpr int NO_POD = 0x7fffffff;
 // walks of up to this many pods run in one wave (k_commit_w): fewer, exact
 // stops for herds on small clusters (C2: 0.67 -> 0.62 ms per pass); longer
@@ -120,6 +120,24 @@ __device__ __forceinline__ void reserve3(int *c0, int *c1, int *c2, int r0, int 
     g2 = reserve<LDS_CAP>(c2, r2);
 }
 
+// The working capacity into LDS by LDS-DMA: one `global_load_lds_dword` per
+// 64 ints (lane-linear), all in flight together, one vmcnt(0) at the end.
+// (A register copy loop, even with 8 loads per thread in flight, made hipcc
+// branch around each load and wait between them: ~30 dependent L2 round trips
+// per thread at 10k nodes for every commit launch.)  Lanes past 3n re-read
+// the last element into the padding of the LDS image (the launch rounds its
+// LDS size up to a 256-byte piece).
+__device__ __forceinline__ void cap_to_lds(const int *g, int *l, int n3, int wave, int n_waves) {
+    const int lane = threadIdx.x & 63;
+    for (int j = wave; j * 64 < n3; j += n_waves) {
+        const int i = min(j * 64 + lane, n3 - 1);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(g + i),
+                                         (void __attribute__((address_space(3))) *)(l + j * 64), 4,
+                                         0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <bool LDS_CAP>
 __global__ void __launch_bounds__(THREADS)
 k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
@@ -153,23 +171,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     } else if (h >= 0) {
         return;
     }
-    if (LDS_CAP) {
-        // 8 loads in flight per thread: a plain copy loop waits out one global
-        // load latency per element (3N / 1024 of them, ~50 us at 10k nodes)
-        for (int i0 = tid; i0 < 3 * N; i0 += 8 * THREADS) {
-            int v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = i0 + u * THREADS;
-                v[u] = i < 3 * N ? cap_g[i] : 0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = i0 + u * THREADS;
-                if (i < 3 * N) capl[i] = v[u];
-            }
-        }
-    }
+    if (LDS_CAP) cap_to_lds(cap_g, capl, 3 * N, tid >> 6, THREADS / 64);
     int *cap = LDS_CAP ? capl : cap_g;
     if (tid == 0) first_bad[0] = first_bad[1] = first_bad[2] = NO_POD;
 
@@ -382,21 +384,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     } else if (h >= 0) {
         return;
     }
-    if (LDS_CAP) {
-        for (int i0 = lane; i0 < 3 * N; i0 += 8 * 64) {
-            int v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = i0 + u * 64;
-                v[u] = i < 3 * N ? cap_g[i] : 0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int i = i0 + u * 64;
-                if (i < 3 * N) capl[i] = v[u];
-            }
-        }
-    }
+    if (LDS_CAP) cap_to_lds(cap_g, capl, 3 * N, 0, 1);
     int *cap = LDS_CAP ? capl : cap_g;
     struct Pod {
         u64 k[KC];
@@ -541,7 +529,7 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
     if (Pp <= ONE_WAVE_MAX_PODS) {
         if (N <= LDS_CAP_MAX_NODES) {
-            const size_t lds = 3 * (size_t)N * 4;
+            const size_t lds = round_up(3 * (size_t)N * 4, 256);  // cap_to_lds pieces
             static std::atomic<unsigned long long> attr{0};
             hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit_w<true>),
                                         LDS_DYN_MAX, attr);
@@ -555,7 +543,7 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
         return hipGetLastError();
     }
     if (N <= LDS_CAP_MAX_NODES) {
-        const size_t lds = 3 * (size_t)N * 4;
+        const size_t lds = round_up(3 * (size_t)N * 4, 256);  // cap_to_lds pieces
         static std::atomic<unsigned long long> attr{0};
         hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit<true>), LDS_DYN_MAX, attr);
         if (e != hipSuccess) return e;
