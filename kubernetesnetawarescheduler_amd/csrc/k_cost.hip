@@ -102,9 +102,20 @@ struct Mma<NAS_DT_BF16> {
     }
 };
 
+// cache policy of the LDS-DMA loads per operand (build-time knob for
+// tools/mb_aux.hip; gfx950 CPol bits: 1 sc0, 2 nt, 16 sc1).  Measured round 2
+// (same box, alternating): sc1 / sc0 sc1 equal to the default within 1%, nt
+// on the traffic rows +5%, on both operands +15-30% -- default kept.
+#ifndef COST_AUX_A
+#define COST_AUX_A 0
+#endif
+#ifndef COST_AUX_B
+#define COST_AUX_B 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void *g, void *l) {
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)g,
-                                     (void __attribute__((address_space(3))) *)l, 16, 0, 0);
+                                     (void __attribute__((address_space(3))) *)l, 16, 0, AUX);
 }
 
 __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
@@ -231,7 +242,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         const int r0 = (j * 8 + w) * 8;
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
-        glds16(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
+        glds16<COST_AUX_A>(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
     };
     int bpod[4];  // RMAP: the WA rows of this lane's four B pieces
     if constexpr (RMAP) {
@@ -244,7 +255,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
         const unsigned char *src = RMAP ? WA + (size_t)bpod[j] * Kb : Bg + (size_t)row * Kb;
-        glds16(src + k0 + c * 16, bbuf(buf) + r0 * BKB);
+        glds16<COST_AUX_B>(src + k0 + c * 16, bbuf(buf) + r0 * BKB);
     };
     auto stageA = [&](int buf, int k0) {
 #pragma unroll
