@@ -1590,8 +1590,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // one launch: halt = -1, rescores / rounds / slot control = 0 (and the
     // published capacity for the L2 commit) -- three memsets and a copy cost
     // ~60 us of serial enqueue before the first chunk
-    HIPCK(nas::launch_pass_init(st, halt, live_cap ? nullptr : ctx->cap.as<int32_t>(),
-                                live_cap ? nullptr : ctx->cap_snap.as<int32_t>(), 3 * N));
+    auto pass_init = [&](hipStream_t s) -> int {
+        HIPCK(nas::launch_pass_init(s, halt, live_cap ? nullptr : ctx->cap.as<int32_t>(),
+                                    live_cap ? nullptr : ctx->cap_snap.as<int32_t>(), 3 * N));
+        return NAS_OK;
+    };
     int32_t *hs = ctx->host_status.as<int32_t>();
     int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
     const bool want_raw = cost_out || int_score_out;
@@ -1613,6 +1616,16 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // (C1 extended 0.41 -> 0.385 ms per nas_place)
     const bool one_stream = chunks.size() == 1 && !ctx->comm;
     if (one_stream) sc = st;
+    // With the LDS commit nothing the scoring kernels read comes from the
+    // pass init (capacity is read live), so the first chunk's fit and cost are
+    // the first launches of the pass and the init goes to the commit stream
+    // behind the scoring enqueues (C3: the first cost launch started ~45 us
+    // after the init, host enqueue time).  The L2 commit's scoring reads the
+    // published copy the init makes: init first, on st.  Either way the other
+    // streams start behind st's work so far -- the inputs prepared on st
+    // above (overflow lists, latency rows, fp32 splits) are read by every
+    // chunk's cost launch.
+    if (!live_cap) OK(pass_init(st));
     if (!one_stream) {
         hipEvent_t ready = tm.mark(st);
         HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
@@ -1629,29 +1642,43 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         OK(score_range(ctx, tm, chunks[c].first, chunks[c].second, ss, score_cap, nullptr, false));
         scored[c] = tm.mark(ss);
     }
+    if (live_cap) OK(pass_init(sc));
     for (size_t c = 0; c < chunks.size(); ++c) {
         const int lo = chunks[c].first, hi = chunks[c].second;
-        HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
-        OK(merge_range(ctx, tm, lo, hi, sc, ctx->comm_c, 0, main_view(ctx)));
-        hipEvent_t c0 = tm.fine(sc);
-        HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+        // the last chunk is merged and committed on its own scoring stream
+        // behind the commit stream's earlier work (long finished by then), so
+        // the pass's serial tail after the last cost launch has no
+        // cross-stream hop in front of its merge (the communicator is the
+        // commit stream's: its collectives stay in one order)
+        const bool tail = !one_stream && c + 1 == chunks.size();
+        hipStream_t cs = sc;
+        if (tail) {
+            cs = (c & 1) ? ctx->stream2 : st;
+            HIPCK(hipStreamWaitEvent(cs, tm.mark(sc), 0));
+        } else {
+            HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
+        }
+        OK(merge_range(ctx, tm, lo, hi, cs, ctx->comm_c, 0, main_view(ctx)));
+        hipEvent_t c0 = tm.fine(cs);
+        HIPCK(nas::launch_commit(cs, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
                                  1, pub));
-        tm.span(T_COMMIT, c0, tm.fine(sc));
+        tm.span(T_COMMIT, c0, tm.fine(cs));
         // this chunk's results go to the pinned stage right behind its
         // commit, and the host unpacks them while later chunks still run
         HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo, (size_t)(hi - lo) * 4,
-                             hipMemcpyDeviceToHost, sc));
+                             hipMemcpyDeviceToHost, cs));
         if (want_raw)
             HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
-                                 (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, sc));
-        landed.push_back({lo, hi, tm.mark(sc)});
+                                 (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, cs));
+        landed.push_back({lo, hi, tm.mark(cs)});
     }
-    if (!one_stream) {
+    // st must follow everything: the last chunk's stream followed the commit
+    // stream, which followed every earlier chunk's scoring; so st waits only
+    // when the last chunk ran on stream2
+    if (!one_stream && chunks.size() % 2 == 0)
         HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
-        HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
-    }
     if (ctx->comm) inject_stall(ctx, st);  // behind every collective of the pass
     // speculative slots: as many as the previous pass of this shape needed
     // (consecutive passes over similar clusters stop alike), enqueued before
@@ -1668,10 +1695,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
                                  st));
     }
     hipEvent_t t1 = nullptr;
+    // status words in one copy: halt[0..2] = halt word, slot resumes, commit
+    // rounds; halt[STATUS_INTS + 2] (slot control) = pods rescored
+    constexpr int NSTAT = nas::STATUS_INTS + 3, RESCORED = nas::STATUS_INTS + 2;
     auto fetch = [&]() -> int {
-        // halt[0..2]: halt word, slot resumes, commit rounds; ctl[2]: pods rescored
-        HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
-        HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(hs, halt, NSTAT * 4, hipMemcpyDeviceToHost, st));
         HIPCK(hipMemcpyAsync(stage, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
         if (want_raw)
             HIPCK(hipMemcpyAsync(stage + P, ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost,
@@ -1695,8 +1723,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // host unpacks each chunk as its copy lands.  Values copied behind a commit
     // are final unless the walk halted there -- then (rare) more slots run and
     // everything is fetched and unpacked again.
-    HIPCK(hipMemcpyAsync(hs, halt, 3 * 4, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(hs + 3, halt + nas::STATUS_INTS + 2, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hs, halt, NSTAT * 4, hipMemcpyDeviceToHost, st));
     t1 = tm.mark(st);
     for (const Landed &l : landed) {
         OK(wait_event(ctx, l.ev));
@@ -1730,7 +1757,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     ctx->timings.commit_ms = tm.total(T_COMMIT);
     ctx->timings.total_ms = tm.total(T_TOTAL);
     ctx->timings.rescore_rounds = hs[1];
-    ctx->timings.rescored_pods = hs[3];
+    ctx->timings.rescored_pods = hs[RESCORED];
     ctx->timings.unschedulable = unsched;
     ctx->timings.commit_rounds = hs[2];
     ctx->slot_hint = std::min(hs[1], MAX_SPEC_SLOTS);
