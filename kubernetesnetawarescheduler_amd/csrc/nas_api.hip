@@ -755,7 +755,10 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
         // the first part would be a sliver of under 16)
         if (c > 0 && left > 32 && left <= big && left - 32 >= 16) tiles = left - 32;
     } else if (mode == 2 && c > 0) {
-        // the rest in equal chunks of at most `big` tiles
+        // the rest in equal chunks of at most `big` tiles (a short last chunk
+        // of 16 / 32 tiles, to shorten the commit left after the scoring,
+        // measured 7-13% slower at G = 8 and 2-3% at G = 4: one more chunk
+        // costs more cross-stream hops than its shorter commit saves)
         const int n = (left + big - 1) / big;
         tiles = (left + n - 1) / n;
     }  // (decreasing chunk sizes n, n-1, ..., 1 measured 7-10% slower at G = 4 / 8)
