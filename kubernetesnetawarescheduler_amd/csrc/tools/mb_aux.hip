@@ -4,6 +4,7 @@
 // Build one binary per knob setting (tools/mb_aux.sh) and run them alternately
 // on one box: prints "<tag> <variant> <ms>" per launch.
 #include "../k_cost.hip"
+#include "k_cost_pc.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -33,9 +34,10 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(WA, h.data(), (size_t)Pp * Kp, hipMemcpyHostToDevice));
     CK(hipMemcpy(Lt, h.data(), (size_t)Mp * Kp, hipMemcpyHostToDevice));
     CK(hipMemset(mask, 0xff, (size_t)(Mp / 64) * Pp * 8));
-    struct V { const char *name; const void *fn; };
-    const V vars[] = {{"top4", (const void *)&k_cost_topk<NAS_DT_I8, 0, 0, 0, -4, false>},
-                      {"noepi", (const void *)&k_cost_topk<NAS_DT_I8, 1, 0, 0, -4, false>}};
+    struct V { const char *name; const void *fn; int threads; };
+    const V vars[] = {{"top4", (const void *)&k_cost_topk<NAS_DT_I8, 0, 0, 0, -4, false>, THREADS},
+                      {"noepi", (const void *)&k_cost_topk<NAS_DT_I8, 1, 0, 0, -4, false>, THREADS},
+                      {"pc/noepi", (const void *)&k_cost_pc<1>, PC_THREADS}};
     for (const V &v : vars)
         CK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<0>()));
     const int n_mt = Mp / BM, n_nt = Pp / BN;
@@ -53,7 +55,7 @@ int main(int argc, char **argv) {
     for (int r = 0; r < reps; ++r)
         for (const V &v : vars) {
             CK(hipEventRecord(a));
-            CK(hipLaunchKernel(v.fn, dim3(n_mt * n_nt), dim3(THREADS), args, lds_bytes<0>(), 0));
+            CK(hipLaunchKernel(v.fn, dim3(n_mt * n_nt), dim3(v.threads), args, lds_bytes<0>(), 0));
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms;
