@@ -75,6 +75,22 @@ constexpr int lds_bytes() {
 #ifndef COST_SCHED
 #define COST_SCHED 0
 #endif
+// wave layout of the 256 x 256 tile: NWN = 4 -> 8 waves (2 node halves x 4 pod
+// quarters), each 128 nodes x 64 pods (4 x 2 MFMA tiles, 128 accumulator
+// registers, two waves per SIMD); NWN = 2 -> 4 waves (2 x 2), each 128 nodes x
+// 128 pods (4 x 4 tiles, 256 accumulator registers, one wave per SIMD): half
+// the LDS fragment reads per MFMA (the layout hipBLASLt picks for this shape,
+// MT256x256, 4 waves; profiles/r02_s3_vendor_gemm_kernels.txt)
+#ifndef COST_NWN_I8
+#define COST_NWN_I8 4
+#endif
+#ifndef COST_NWN_BF16
+#define COST_NWN_BF16 4
+#endif
+template <int DT>
+constexpr int cost_nwn() {
+    return DT == NAS_DT_I8 ? COST_NWN_I8 : COST_NWN_BF16;
+}
 
 template <int DT>
 struct Mma;
@@ -159,14 +175,20 @@ struct Top4 {
 // (read in place by the LDS-DMA source addresses; rows past the view's count
 // read its last row and are never merged)
 template <int DT, int EPI = 0, int SCHED = COST_SCHED, int PIPE = COST_PIPE, int GM = COST_GM,
-          bool RMAP = false>
-__global__ void __launch_bounds__(THREADS, 1)
+          bool RMAP = false, int NWN = 4>
+__global__ void __launch_bounds__(128 * NWN, 1)
 k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
             u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base,
             const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
             Ovf ov, const int *__restrict__ rowmap) {
     static_assert(!RMAP || PIPE == 0, "the row map is wired into the LDS-DMA staging only");
+    static_assert(NWN == 4 || (NWN == 2 && PIPE == 0 && (SCHED == 0 || SCHED == 2)),
+                  "the 4-wave layout has the two-stage LDS-DMA pipeline only");
+    constexpr int NW = 2 * NWN;     // waves
+    constexpr int NI = 8 / NWN;     // 32-pod MFMA tiles per wave
+    constexpr int WPODS = 32 * NI;  // pods per wave
+    constexpr int PPW = 32 / NW;    // 1 KiB LDS-DMA pieces per operand per wave per stage
     using M = Mma<DT>;
     using acc_t = typename M::acc_t;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -212,7 +234,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     }
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wm = w >> 2, wn = w & 3;
+    const int wm = w / NWN, wn = w % NWN;
 
     const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
     const unsigned char *Bg = WA + (size_t)(p0 + nt * BN) * Kb;
@@ -221,7 +243,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         Bg = WA;
     }
 
-    // LDS-DMA staging: piece j of wave w fills rows (8j + w)*8 .. +8 of A
+    // LDS-DMA staging: piece j of wave w fills rows (NW*j + w)*8 .. +8 of A
     // and of B (1 KiB each, lane-linear: lane l -> row + l/8, 16-byte chunk
     // l%8; whole 128-byte lines per row -- 64-byte row pieces measured 12%
     // slower); the chunk swizzle chunk ^= (row >> 1) & 7 is applied on the
@@ -237,21 +259,21 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         return PIPE != 1 ? lds + b * STAGE_BYTES + TILE_BYTES : lds + (2 + b) * TILE_BYTES;
     };
     // one 1 KiB LDS-DMA piece (8 rows x 128 B) of operand A / B: piece j of
-    // wave w fills rows (8j + w)*8 .. +8
+    // wave w fills rows (NW*j + w)*8 .. +8
     auto pieceA = [&](int buf, int k0, int j) {
-        const int r0 = (j * 8 + w) * 8;
+        const int r0 = (j * NW + w) * 8;
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
         glds16<COST_AUX_A>(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
     };
-    int bpod[4];  // RMAP: the WA rows of this lane's four B pieces
+    int bpod[PPW];  // RMAP: the WA rows of this lane's B pieces
     if constexpr (RMAP) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            bpod[j] = rowmap[min(p0 + nt * BN + (j * 8 + w) * 8 + srow_in, dyn_hi - 1)];
+        for (int j = 0; j < PPW; ++j)
+            bpod[j] = rowmap[min(p0 + nt * BN + (j * NW + w) * 8 + srow_in, dyn_hi - 1)];
     }
     auto pieceB = [&](int buf, int k0, int j) {
-        const int r0 = (j * 8 + w) * 8;
+        const int r0 = (j * NW + w) * 8;
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
         const unsigned char *src = RMAP ? WA + (size_t)bpod[j] * Kb : Bg + (size_t)row * Kb;
@@ -259,31 +281,31 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     };
     auto stageA = [&](int buf, int k0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) pieceA(buf, k0, j);
+        for (int j = 0; j < PPW; ++j) pieceA(buf, k0, j);
     };
     auto stageB = [&](int buf, int k0) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) pieceB(buf, k0, j);
+        for (int j = 0; j < PPW; ++j) pieceB(buf, k0, j);
     };
 
     // the epilogue's fit-mask words, loaded now so their latency hides
     // under the main loop (k_fit wrote them before this launch)
-    u64 mwp[2][2];
+    u64 mwp[NI][2];
     if constexpr (EPI == 0 || EPI == 2 || EPI == 6) {
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
+        for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
             for (int mi2 = 0; mi2 < 2; ++mi2) {
-                const int pod = p0 + nt * BN + wn * 64 + ni * 32 + (lane & 31);
+                const int pod = p0 + nt * BN + wn * WPODS + ni * 32 + (lane & 31);
                 const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
                 mwp[ni][mi2] = mask[(size_t)chunk * Pp + pod];
             }
     }
-    acc_t acc[4][2];
+    acc_t acc[4][NI];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = acc_t{};
+        for (int j = 0; j < NI; ++j) acc[i][j] = acc_t{};
     const int fr = lane & 31, fh = lane >> 5;
     // ---- exact int32 traffic: the entries outside the int8 plane (nas::Ovf):
     // e * L[m][n] for the lane's 64 nodes per pod are the accumulators'
@@ -294,8 +316,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
             const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
 #pragma unroll
-            for (int ni = 0; ni < 2; ++ni) {
-                const int r = p0 + nt * BN + wn * 64 + ni * 32 + (lane & 31);
+            for (int ni = 0; ni < NI; ++ni) {
+                const int r = p0 + nt * BN + wn * WPODS + ni * 32 + (lane & 31);
                 int beg = 0, end = 0;
                 if (r < cnt_lim) {
                     const int pod = (ov.row_pod ? ov.row_pod[r] : r) + cb * Pp;
@@ -328,8 +350,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     auto compute = [&](int ab, int bbi, auto &&piece) {
         const unsigned char *As = abuf(ab);
         const unsigned char *Bs = bbuf(bbi);
-        v4i a[2][4], bb[2][2];
-        auto read = [&](int kk, v4i (&ra)[4], v4i (&rb)[2]) {
+        v4i a[2][4], bb[2][NI];
+        auto read = [&](int kk, v4i (&ra)[4], v4i (&rb)[NI]) {
             const int c = kk * 2 + fh;
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
@@ -337,8 +359,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                 ra[mi] = *reinterpret_cast<const v4i *>(As + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
             }
 #pragma unroll
-            for (int ni = 0; ni < 2; ++ni) {
-                const int r = wn * 64 + ni * 32 + fr;
+            for (int ni = 0; ni < NI; ++ni) {
+                const int r = wn * WPODS + ni * 32 + fr;
                 rb[ni] = *reinterpret_cast<const v4i *>(Bs + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
             }
         };
@@ -351,7 +373,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                for (int ni = 0; ni < 2; ++ni)
+                for (int ni = 0; ni < NI; ++ni)
                     acc[mi][ni] = M::mma(a[kk & 1][mi], bb[kk & 1][ni], acc[mi][ni]);
             if constexpr (SCHED == 2) __builtin_amdgcn_s_setprio(0);
             if constexpr (SCHED == 1) {
@@ -630,7 +652,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < 2; ++ni) {
+            for (int ni = 0; ni < NI; ++ni) {
 #if defined(__HIP_DEVICE_COMPILE__)
                 asm volatile("" ::"v"(acc[mi][ni]));
 #endif
@@ -641,9 +663,9 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // per lane: top-4 of its 64 (node, cost) values per pod; lanes l and l^32
     // (same pod, complementary rows) merge into a sorted 8-list whose bound is
     // the smaller of the two 4th keys (every key <= bound is in the list)
-    u64 key[2][8], bnd[2];
+    u64 key[NI][8], bnd[NI];
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
+    for (int ni = 0; ni < NI; ++ni) {
         const u64 *mw = mwp[ni];
         // orderable keys of the lane's 64 (node, cost) values and their range
         // (int8: the range of the raw int32 costs -- the key is x ^ 2^31, so
@@ -752,8 +774,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     u64 *xk = reinterpret_cast<u64 *>(lds);  // [wn][ni][32][9], staging is dead
     if (wm == 1 && fh == 0) {
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-            u64 *d = xk + ((wn * 2 + ni) * 32 + fr) * 9;
+        for (int ni = 0; ni < NI; ++ni) {
+            u64 *d = xk + ((wn * NI + ni) * 32 + fr) * 9;
 #pragma unroll
             for (int j = 0; j < 8; ++j) d[j] = key[ni][j];
             d[8] = bnd[ni];
@@ -761,22 +783,25 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     }
     __syncthreads();
     if (wm == 0) {
-        // lane < 32 -> pods wn*64 + 0..31 (ni = 0), lane >= 32 -> +32..63 (ni = 1);
-        // two constant-index branches, not key[fh][j] (a runtime index puts
-        // the lists in scratch)
-        auto finish = [&](u64 (&mine)[8], u64 b, int ni) {
+        // round rr: lane < 32 -> pods wn*WPODS + 64rr + 0..31 (ni = 2rr), lane >=
+        // 32 -> +32..63 (ni = 2rr + 1); constant-index branches, not key[fh][j]
+        // (a runtime index puts the lists in scratch)
+        auto finish = [&](u64 (&mine)[8], u64 b, int ni, int rr) {
             u64 other[8];
-            const u64 *s = xk + ((wn * 2 + ni) * 32 + fr) * 9;
+            const u64 *s = xk + ((wn * NI + ni) * 32 + fr) * 9;
 #pragma unroll
             for (int j = 0; j < 8; ++j) other[j] = s[j];
             merge88(mine, other);
             b = umin64(umin64(b, s[8]), mine[7]);
-            const int pod = p0 + nt * BN + wn * 64 + lane;
+            const int pod = p0 + nt * BN + wn * WPODS + rr * 64 + lane;
             store8(partial + ((size_t)mt * Pp + pod) * KC, mine);
             pbound[(size_t)mt * Pp + pod] = b;
         };
-        if (fh == 0) finish(key[0], bnd[0], 0);
-        else finish(key[1], bnd[1], 1);
+#pragma unroll
+        for (int rr = 0; rr < NI / 2; ++rr) {
+            if (fh == 0) finish(key[2 * rr], bnd[2 * rr], 2 * rr, rr);
+            else finish(key[2 * rr + 1], bnd[2 * rr + 1], 2 * rr + 1, rr);
+        }
     }
 }
 
@@ -861,8 +886,9 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
                          int p0, int np, const uint64_t *mask, uint64_t *partial,
                          uint64_t *pbound, int node_base, const Dyn *dyn, int batch,
                          const Ovf &ov, const int32_t *rowmap) {
+    constexpr int NWN = cost_nwn<DT>();
     const void *fn = reinterpret_cast<const void *>(
-        &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP>);
+        &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP, NWN>);
     const int lds = lds_bytes<COST_PIPE>();
     static std::atomic<unsigned long long> attr_set{0};
     hipError_t e = set_lds_once(fn, lds, attr_set);
@@ -876,7 +902,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const int *ds = dyn ? dyn->start : nullptr;
     const int dh = dyn ? dyn->hi : 0;
     const int *dhp = dyn ? dyn->hi_ptr : nullptr;
-    k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP><<<dim3(n_mt * n_nt, batch), THREADS, lds, st>>>(
+    k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP, NWN><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
         lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dh, dhp, ov, rowmap);
     return hipGetLastError();
 }

@@ -4,10 +4,10 @@
 // Build one binary per knob setting (tools/mb_aux.sh) and run them alternately
 // on one box: prints "<tag> <variant> <ms>" per launch.
 #include "../k_cost.hip"
-#include "k_cost_pc.hip"
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 using namespace nas;
@@ -34,10 +34,24 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(WA, h.data(), (size_t)Pp * Kp, hipMemcpyHostToDevice));
     CK(hipMemcpy(Lt, h.data(), (size_t)Mp * Kp, hipMemcpyHostToDevice));
     CK(hipMemset(mask, 0xff, (size_t)(Mp / 64) * Pp * 8));
-    struct V { const char *name; const void *fn; int threads; };
-    const V vars[] = {{"top4", (const void *)&k_cost_topk<NAS_DT_I8, 0, 0, 0, -4, false>, THREADS},
-                      {"noepi", (const void *)&k_cost_topk<NAS_DT_I8, 1, 0, 0, -4, false>, THREADS},
-                      {"pc/noepi", (const void *)&k_cost_pc<1>, PC_THREADS}};
+    // bf16 operands (C3-like: latency 1..105, traffic 0..2, as bf16 values)
+    void *Ltb, *WAb;
+    CK(hipMalloc(&Ltb, (size_t)Mp * Kp * 2));
+    CK(hipMalloc(&WAb, (size_t)Pp * Kp * 2));
+    {
+        std::vector<unsigned short> hb((size_t)Pp * Kp);
+        auto bf = [](float f) { unsigned u; memcpy(&u, &f, 4); return (unsigned short)(u >> 16); };
+        for (size_t i = 0; i < hb.size(); ++i) hb[i] = bf((float)((i * 2654435761u >> 13) % 3));
+        CK(hipMemcpy(WAb, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+        for (size_t i = 0; i < (size_t)Mp * Kp; ++i) hb[i] = bf((float)(1 + (i * 2246822519u >> 11) % 105));
+        CK(hipMemcpy(Ltb, hb.data(), (size_t)Mp * Kp * 2, hipMemcpyHostToDevice));
+    }
+    struct V { const char *name; const void *fn; int threads; bool b16; };
+    const V vars[] = {{"top4", (const void *)&k_cost_topk<NAS_DT_I8, 0, 0, 0, -4, false, 4>, 512, false},
+                      {"top4/w4", (const void *)&k_cost_topk<NAS_DT_I8, 0, 0, 0, -4, false, 2>, 256, false},
+                      {"noepi/w4", (const void *)&k_cost_topk<NAS_DT_I8, 1, 0, 0, -4, false, 2>, 256, false},
+                      {"bf16/top4", (const void *)&k_cost_topk<NAS_DT_BF16, 0, 0, 0, -4, false, 4>, 512, true},
+                      {"bf16/top4/w4", (const void *)&k_cost_topk<NAS_DT_BF16, 0, 0, 0, -4, false, 2>, 256, true}};
     for (const V &v : vars)
         CK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes<0>()));
     const int n_mt = Mp / BM, n_nt = Pp / BN;
@@ -45,6 +59,8 @@ int main(int argc, char **argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     const unsigned char *lt = (const unsigned char *)Lt, *wa = (const unsigned char *)WA;
+    const unsigned char *ltb = (const unsigned char *)Ltb, *wab = (const unsigned char *)WAb;
+    const int Kb2 = 2 * Kp;
     const u64 *mk = (const u64 *)mask;
     u64 *pa = (u64 *)partial, *pb = (u64 *)pbound;
     int zero = 0;
@@ -52,10 +68,15 @@ int main(int argc, char **argv) {
     Ovf noovf{};
     void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero, (void *)&Pp, &mk,
                     &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf, &nodyn};
+    void *argsb[] = {&ltb, &wab, (void *)&Kb2, (void *)&n_mt, (void *)&n_nt, &zero, (void *)&Pp, &mk,
+                     &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf, &nodyn};
+    const char *sel = argc > 4 ? argv[4] : nullptr;  // substring filter on variant names
     for (int r = 0; r < reps; ++r)
         for (const V &v : vars) {
+            if (sel && !strstr(v.name, sel)) continue;
             CK(hipEventRecord(a));
-            CK(hipLaunchKernel(v.fn, dim3(n_mt * n_nt), dim3(v.threads), args, lds_bytes<0>(), 0));
+            CK(hipLaunchKernel(v.fn, dim3(n_mt * n_nt), dim3(v.threads), v.b16 ? argsb : args,
+                               lds_bytes<0>(), 0));
             CK(hipEventRecord(b));
             CK(hipEventSynchronize(b));
             float ms;
