@@ -261,6 +261,59 @@ def bench_cost_kernel(args, d, eng):
     return float(np.mean(ms)), ms
 
 
+def vendor_gemm_reference(args, d, reps=5):
+    """Known-good ceiling reference for the dominant kernel, measured in this
+    run (cdna_hip_programming.md §5.4 rule 10): the vendor library's plain
+    GEMM (hipBLASLt through torch._int_mm / torch.matmul) at the shape
+    k_cost_topk launches -- Mp x Kp nodes x K, Pp pods, both operands
+    K-contiguous -- on operands with the C3 value ranges (latency 1..105,
+    traffic 0..2).  The library writes the whole product to HBM (int32 4.1 GB
+    at C3); k_cost_topk fuses the fit mask and the top-8 reduction instead.
+    `frac` uses the same 2*P*N*N_local op count as the roofline object, so the
+    two fractions compare directly.  Not the product path: a measurement aid."""
+    import torch
+    N, P = args.nodes, args.pods
+    nloc = N // max(d.world, args.rehearse_world)
+    r = lambda x, m: (x + m - 1) // m * m  # noqa: E731
+    M, K, Pp = r(nloc, 256), r(N, 128 if args.dtype == "i8" else 64), r(P, 256)
+    dev = torch.device("cuda", d.local)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED)
+    A = torch.randint(1, 106, (M, K), generator=g, device=dev, dtype=torch.int32).to(torch.int8)
+    Bt = torch.randint(0, 3, (Pp, K), generator=g, device=dev, dtype=torch.int32).to(torch.int8)
+    if args.dtype == "i8":
+        B = Bt.t()  # [K][Pp] view of the pod rows: K contiguous, as WA is stored
+        fn = lambda: torch._int_mm(A, B)  # noqa: E731
+        lib, peak = "hipBLASLt int8 GEMM (torch._int_mm), int32 output", PEAK_I8_TOPS
+    else:
+        A, B = A.to(torch.bfloat16), Bt.to(torch.bfloat16).t()
+        fn = lambda: torch.matmul(A, B)  # noqa: E731
+        lib, peak = "hipBLASLt bf16 GEMM (torch.matmul), bf16 output", PEAK_BF16_TFLOPS
+    try:
+        fn()
+        torch.cuda.synchronize()
+        ms = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        ms_mean = float(np.mean(ms))
+        ops = 2.0 * P * N * nloc
+        return {"library": lib, "shape": {"nodes": M, "k": K, "pods": Pp},
+                "launch_ms": ms_mean, "launch_ms_min": min(ms), "launches": reps,
+                "achieved": ops / (ms_mean * 1e-3) / 1e12, "frac": ops / (ms_mean * 1e-3) / 1e12 / peak,
+                "note": "plain GEMM, whole product stored to HBM, C3 value ranges; same op count "
+                        "and peak as the roofline object"}
+    except Exception as e:  # noqa: BLE001 -- a library refusal is reported, not fatal
+        return {"library": lib, "error": str(e)[:200]}
+    finally:
+        del A, Bt, B
+        torch.cuda.empty_cache()
+
+
 def bench_vote(args, d, eng):
     N = args.nodes
     if args.vote_node_shard:
@@ -734,6 +787,8 @@ def main():
                                    "this rank's node columns (nas_score), HIP events on its "
                                    "stream; 2*P*N*N_local ops; tools/check_roofline.py compares "
                                    "it with the rocprofv3 kernel trace of the same command"}
+        if d.gpu and d.world == 1 and args.only is None:
+            out["roofline"]["vendor_gemm"] = vendor_gemm_reference(args, d)
     if traffic.get("k_fit"):
         fb = 2.0 * N * 4 * 3 + 2.0 * P * 4 * 3 + P * ((N + 63) // 64) * 8.0  # capacities, requests, mask
         out["fit_traffic"] = {"kernel": "k_fit", "bytes": traffic["k_fit"]["bytes"],
