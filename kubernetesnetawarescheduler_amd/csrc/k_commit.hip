@@ -37,6 +37,18 @@
 // The L2 form's speculative reservations can dip below the committed state, so
 // it also subtracts each committed pod from `pub` (when given): a published
 // capacity that is always >= the working one, for concurrent scoring to read.
+//
+// Zero-traffic pods (zrow[p] = 1: no traffic to any bound peer, so every cost
+// is exactly 0 and key order is node order): the list holds the lowest-index
+// nodes that fitted when it was scored, and every node up to the bound's node
+// is either in the list or did not fit then (capacity only shrinks).  When
+// none of its usable candidates fits, such a pod's sequential choice is the
+// first node ABOVE the bound's node that fits now -- found by a scan of the
+// capacity instead of a rescore; a scan that reaches the last node without a
+// fit means no node fits (NAS_EMPTY).  A herd of such pods (pods with no
+// placed peers) fills the nodes in index order, and without the scan drains
+// one 8-node list per rescore slot (C2: 5 slots, 1,087 of its 1,654
+// zero-traffic pods land outside their first list).
 #include "klist.h"
 
 namespace nas {
@@ -44,7 +56,31 @@ namespace {
 
 constexpr int THREADS = 1024;  // one window of pods per round
 constexpr int LDS_DYN_MAX = 160 * 1024 - 512;  // leaves room for the static LDS
-constexpr int LDS_CAP_MAX_NODES = (LDS_DYN_MAX - 256) / 12;  // + cap_to_lds padding
+// k_commit_w's prefetch ring of candidate lists in LDS (after the capacity):
+// PF_SLOTS windows of 64 pods, PF_SLOT bytes each -- keys [64][8] u64 at 0,
+// bounds [64] u64 at 4096 (+512 written by the idle half of the wave), requests
+// [3][64] int32 at 5120, zero-traffic flags [64] bytes at 5888 (+192 idle)
+constexpr int PF_SLOT = 6144;
+constexpr int PF_SLOTS = 4;
+constexpr int PF_BYTES = PF_SLOT * PF_SLOTS;
+constexpr int PF_LOADS = 9;  // LDS-DMA instructions per window
+// build-time knobs (A/B'd on one box): windows in flight beyond
+// the walked one (1..3), the zero-traffic scan, the batched candidate reads
+#ifndef COMMIT_AHEAD
+#define COMMIT_AHEAD 3
+#endif
+#ifndef COMMIT_ZSCAN
+#define COMMIT_ZSCAN 1
+#endif
+#ifndef COMMIT_BATCH
+#define COMMIT_BATCH 1
+#endif
+static_assert(COMMIT_AHEAD >= 1 && COMMIT_AHEAD < PF_SLOTS, "ring depth");
+template <int N>
+__device__ __forceinline__ void retire_window();
+// retire the oldest window in flight while `younger` (0..3) later ones stay
+__device__ __forceinline__ void retire_oldest(int younger);
+constexpr int LDS_CAP_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 12;  // + cap_to_lds padding
 constexpr int NO_POD = 0x7fffffff;
 // walks of up to this many pods run in one wave (k_commit_w): fewer, exact
 // stops for herds on small clusters (C2: 0.67 -> 0.62 ms per pass); longer
@@ -60,6 +96,37 @@ constexpr int ONE_WAVE_MAX_PODS = 16384;
 // above INT_MIN (1024 * 2^21 = 2^31).  Larger requests keep the CAS loop,
 // which never takes a resource below zero.
 constexpr int FETCH_SUB_MAX = 1 << 21;
+
+// the orderable encoding of cost 0 (int8: 0 ^ 2^31; bf16 / fp32: +0 with the
+// sign bit set), the high word of every key of a zero-traffic pod
+constexpr unsigned ZERO_COST_KEY = 0x80000000u;
+// nodes a zero-traffic pick scans past its list (capacity in LDS / in L2);
+// a longer walk falls back to a rescore
+constexpr int ZSCAN_LDS = 1024;
+constexpr int ZSCAN_L2 = 16;
+
+// A zero-traffic pod whose usable candidates are all full: the first node
+// above its bound's node that fits the capacity read by `ld`.  Returns the
+// node, -1 when no node fits at all (the scan reached N), or -2 when the scan
+// limit ran out first (rescore).
+template <bool LDS_CAP, typename LD>
+__device__ __forceinline__ int zero_row_scan(u64 bound, int r0, int r1, int r2, int N, LD &&ld) {
+    const int n0 = (int)(unsigned)bound + 1;
+    const int n1 = min(N, n0 + (LDS_CAP ? ZSCAN_LDS : ZSCAN_L2));
+    // 8 nodes per step, their 24 reads in flight together (a node past n1
+    // re-reads n1 - 1 and is never taken)
+    for (int n = n0; n < n1; n += 8) {
+        unsigned fit = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int m = min(n + j, n1 - 1);
+            const int a = ld(m), b = ld(N + m), c = ld(2 * N + m);
+            fit |= (unsigned)((r0 <= a) & (r1 <= b) & (r2 <= c) & (n + j < n1)) << j;
+        }
+        if (fit) return n + __builtin_ctz(fit);
+    }
+    return n1 == N ? -1 : -2;
+}
 
 // reserve r from *c iff *c >= r; returns success
 template <bool LDS_CAP>
@@ -143,7 +210,7 @@ __global__ void __launch_bounds__(THREADS)
 k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
          const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
          int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
-         int *__restrict__ halt, int *__restrict__ pub) {
+         int *__restrict__ halt, int *__restrict__ pub, const unsigned char *__restrict__ zrow) {
     // one workgroup per cluster of a batched launch
     const int cb = blockIdx.x;
     cand_key += (size_t)cb * Pp * KC;
@@ -154,6 +221,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     out_cost += (size_t)cb * Pp;
     halt += cb * STATUS_INTS;
     if (pub) pub += (size_t)cb * 3 * N;
+    if (zrow) zrow += (size_t)cb * Pp;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     __shared__ int first_bad[3];  // round r uses slot r % 3
     __shared__ int s_rescore;     // the round's lowest bad pod needs a rescore
@@ -240,7 +308,15 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 }
             }
             if (done) choice = -1;
-            const bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
+            bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
+            if (COMMIT_ZSCAN && rescore && zrow && zrow[i] && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
+                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld);
+                if (z != -2) {
+                    rescore = false;
+                    choice = z;  // -1: nothing fits (NAS_EMPTY)
+                    ccost = ZERO_COST_KEY;
+                }
+            }
             // every pick must see the capacity at the START of the round: a
             // later pod's reservation must not push an earlier pod off a node
             round_barrier<LDS_CAP>();
@@ -328,34 +404,46 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
 // depends on that order (the argument of step 3 holds for any atomic order);
 // only the number of rounds does.
 // ---------------------------------------------------------------------------
-// The next window's lists are prefetched by inline-asm loads the compiler's
-// waitcnt pass does not track, retired by one vmcnt(0) tied to every
-// destination register just before the window starts: with compiler-visible
-// loads hipcc waits for the prefetch right where it is issued (the loop-carried
-// registers look pending), and every window pays a full load latency.
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
-struct PodRaw {
-    v4u k0, k1, k2, k3;
-    u64 bound;
-    int r0, r1, r2;
-};
-__device__ __forceinline__ void prefetch_pod(const u64 *kp, const u64 *bp, const int *q0,
-                                             const int *q1, const int *q2, PodRaw &o) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(o.k0) : "v"(kp) : "memory");
-    asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(o.k1) : "v"(kp) : "memory");
-    asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(o.k2) : "v"(kp) : "memory");
-    asm volatile("global_load_dwordx4 %0, %1, off offset:48" : "=v"(o.k3) : "v"(kp) : "memory");
-    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(o.bound) : "v"(bp) : "memory");
-    asm volatile("global_load_dword %0, %1, off" : "=v"(o.r0) : "v"(q0) : "memory");
-    asm volatile("global_load_dword %0, %1, off" : "=v"(o.r1) : "v"(q1) : "memory");
-    asm volatile("global_load_dword %0, %1, off" : "=v"(o.r2) : "v"(q2) : "memory");
+// The lists of windows k+1 .. k+3 stream into an LDS ring (LDS-DMA) while
+// window k walks: a window's lists were written by k_merge on other XCDs, so
+// every load is a trip beyond L2 (~1-2 us), longer than a window's rounds.
+// LDS-DMA keeps the in-flight data out of registers (a register prefetch
+// across loop iterations lets the compiler copy a pending load's destination
+// before its wait).  The retire waits only for the window it takes.
+template <int N>
+__device__ __forceinline__ void retire_window() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    __builtin_amdgcn_s_barrier();  // (one wave: orders its own LDS-DMA before its reads)
+    asm volatile("" ::: "memory");
 }
-__device__ __forceinline__ void retire_pod(PodRaw &o) {
-    asm volatile("s_waitcnt vmcnt(0)"
-                 : "+v"(o.k0), "+v"(o.k1), "+v"(o.k2), "+v"(o.k3), "+v"(o.bound), "+v"(o.r0),
-                   "+v"(o.r1), "+v"(o.r2)
-                 :
-                 : "memory");
+// LDS-DMA hipcc does not count (cdna_hip_programming.md §5.7 recipe): with the
+// builtin, hipcc drains every outstanding LDS-DMA (vmcnt(0)) before each LDS
+// atomic of the walk, as it cannot tell the ring from the capacity.  `lds` is
+// the wave-uniform LDS byte address; M0 is saved and restored in the statement.
+__device__ __forceinline__ unsigned lds_addr(const void *p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ void retire_oldest(int younger) {
+    if (younger >= 3) retire_window<3 * PF_LOADS>();
+    else if (younger == 2) retire_window<2 * PF_LOADS>();
+    else if (younger == 1) retire_window<PF_LOADS>();
+    else retire_window<0>();
+}
+template <int SZ>
+__device__ __forceinline__ void glds(const void *g, unsigned lds) {
+    unsigned keep;
+    if constexpr (SZ == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(g), "s"(lds)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(g), "s"(lds)
+                     : "memory");
 }
 
 template <bool LDS_CAP>
@@ -363,7 +451,7 @@ __global__ void __launch_bounds__(64)
 k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
            const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
            int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
-           int *__restrict__ halt, int *__restrict__ pub) {
+           int *__restrict__ halt, int *__restrict__ pub, const unsigned char *__restrict__ zrow) {
     const int cb = blockIdx.x;
     cand_key += (size_t)cb * Pp * KC;
     cand_bound += (size_t)cb * Pp;
@@ -373,6 +461,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     out_cost += (size_t)cb * Pp;
     halt += cb * STATUS_INTS;
     if (pub) pub += (size_t)cb * 3 * N;
+    if (zrow) zrow += (size_t)cb * Pp;
     extern __shared__ __attribute__((aligned(16))) int smem[];
     int *capl = smem;
     const int lane = threadIdx.x;
@@ -390,14 +479,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         u64 k[KC];
         u64 bound;
         int r0, r1, r2;
-    };
-    auto load = [&](int base, Pod &c) {  // as k_commit's: pods past p_end are `done`
-        const int ii = min(base + lane, Pp - 1);
-        load8(cand_key + (size_t)ii * KC, c.k);
-        c.bound = cand_bound[ii];
-        c.r0 = req[ii];
-        c.r1 = req[Pp + ii];
-        c.r2 = req[2 * Pp + ii];
+        int z;  // zero-traffic pod (zrow)
     };
     auto publish = [&](int n, const Pod &c) {
         if (LDS_CAP || !pub || n < 0) return;
@@ -410,40 +492,98 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         return __hip_atomic_load(cap + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     Pod cur;
-    PodRaw nxt;
-    load(p_begin, cur);
     if (lane == 0 && h >= 0) {
         halt[0] = -1;
         if (resume) halt[1] += 1;
     }
+    unsigned char *pf = reinterpret_cast<unsigned char *>(smem) + (LDS_CAP ? (3 * N * 4 + 255) / 256 * 256 : 0);
+    const unsigned char *zsrc = zrow ? zrow : reinterpret_cast<const unsigned char *>(req);
+    // window wbase's lists into ring slot `slot` (9 LDS-DMA instructions; lanes
+    // past the data re-read its last bytes into the slot's idle space)
+    auto issue = [&](int wbase, int slot) {
+        if (wbase >= p_end) return;
+        const unsigned d = __builtin_amdgcn_readfirstlane(lds_addr(pf + slot * PF_SLOT));
+        const auto *kb = reinterpret_cast<const unsigned char *>(cand_key);
+        const size_t kmax = (size_t)Pp * KC * 8 - 16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            glds<16>(kb + min((size_t)wbase * KC * 8 + j * 1024 + lane * 16, kmax), d + j * 1024);
+        glds<16>(reinterpret_cast<const unsigned char *>(cand_bound) +
+                     min((size_t)wbase * 8 + lane * 16, (size_t)Pp * 8 - 16),
+                 d + 4096);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) glds<4>(req + (size_t)r * Pp + min(wbase + lane, Pp - 1), d + 5120 + r * 256);
+        glds<4>(zsrc + min(wbase + 4 * lane, Pp - 4), d + 5888);
+    };
+    auto take = [&](int slot) {
+        const unsigned char *d = pf + slot * PF_SLOT;
+        load8(reinterpret_cast<const u64 *>(d) + lane * KC, cur.k);
+        cur.bound = reinterpret_cast<const u64 *>(d + 4096)[lane];
+        cur.r0 = reinterpret_cast<const int *>(d + 5120)[lane];
+        cur.r1 = reinterpret_cast<const int *>(d + 5120 + 256)[lane];
+        cur.r2 = reinterpret_cast<const int *>(d + 5120 + 512)[lane];
+        cur.z = zrow ? (int)d[5888 + lane] : 0;
+    };
+    // windows 0..3 into slots 0..3; window w always sits in slot w % 4
+    int younger = 0;
+    for (int j = 0; j <= COMMIT_AHEAD; ++j) {
+        issue(p_begin + 64 * j, j);
+        younger += j > 0 && p_begin + 64 * j < p_end;
+    }
+    retire_oldest(younger);
+    take(0);
     int round = 0;
     int stop = p_end;
-    for (int base = p_begin; base < p_end; base += 64) {
-        if (base + 64 < p_end) {  // prefetch the next window (untracked loads)
-            const int ii = min(base + 64 + lane, Pp - 1);
-            prefetch_pod(cand_key + (size_t)ii * KC, cand_bound + ii, req + ii, req + Pp + ii,
-                         req + 2 * Pp + ii, nxt);
-        }
+    for (int base = p_begin, w = 0;; ++w) {
         const int i = base + lane;
         bool done = i >= p_end;
         while (true) {
             int choice = -1;
             unsigned ccost = 0;
-            if (!done) {
+            if (!done && COMMIT_BATCH) {
+                // every usable candidate's capacity at once (24 independent LDS
+                // reads, not up to 8 dependent rounds of 3): a herd member whose
+                // first candidates are full costs one LDS latency, not eight.
+                // Keys ascend and the unusable ones (> bound, KEY_INVALID) come
+                // last, so the lowest fitting bit is the sequential choice.
+                unsigned okm = 0;
+#pragma unroll
+                for (int j = 0; j < KC; ++j) {
+                    const u64 k = cur.k[j];
+                    const bool usable = k != KEY_INVALID && k <= cur.bound;
+                    const int n = usable ? (int)(unsigned)k : 0;
+                    const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
+                    okm |= (unsigned)(usable & (cur.r0 <= a) & (cur.r1 <= b) & (cur.r2 <= c)) << j;
+                }
+#pragma unroll
+                for (int j = KC - 1; j >= 0; --j)  // constant indices (no scratch array)
+                    if ((okm >> j) & 1u) {
+                        choice = (int)(unsigned)cur.k[j];
+                        ccost = (unsigned)(cur.k[j] >> 32);
+                    }
+            }
+            if (!done && !COMMIT_BATCH) {
 #pragma unroll
                 for (int j = 0; j < KC; ++j) {
                     const u64 k = cur.k[j];
                     if (k == KEY_INVALID || k > cur.bound) break;
                     const int n = (int)(unsigned)k;
-                    const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
-                    if (cur.r0 <= a && cur.r1 <= b && cur.r2 <= c) {
+                    if (cur.r0 <= ld(n) && cur.r1 <= ld(N + n) && cur.r2 <= ld(2 * N + n)) {
                         choice = n;
                         ccost = (unsigned)(k >> 32);
                         break;
                     }
                 }
             }
-            const bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
+            bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
+            if (COMMIT_ZSCAN && rescore && cur.z && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
+                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld);
+                if (z != -2) {
+                    rescore = false;
+                    choice = z;  // -1: nothing fits (NAS_EMPTY)
+                    ccost = ZERO_COST_KEY;
+                }
+            }
             bool g0 = false, g1 = false, g2 = false;
             if (choice >= 0)
                 reserve3<LDS_CAP>(cap + choice, cap + N + choice, cap + 2 * N + choice, cur.r0,
@@ -491,20 +631,15 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 }
             }
         }
-        if (stop < p_end) break;
-        if (base + 64 < p_end) {
-            retire_pod(nxt);
-            const v4u kk[4] = {nxt.k0, nxt.k1, nxt.k2, nxt.k3};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                cur.k[2 * j] = ((u64)kk[j].y << 32) | kk[j].x;
-                cur.k[2 * j + 1] = ((u64)kk[j].w << 32) | kk[j].z;
-            }
-            cur.bound = nxt.bound;
-            cur.r0 = nxt.r0;
-            cur.r1 = nxt.r1;
-            cur.r2 = nxt.r2;
-        }
+        if (stop < p_end || base + 64 >= p_end) break;
+        // window w+1 (slot (w+1) % 4): windows w+2, w+3 may stay in flight
+        younger = 0;
+        for (int j = 2; j <= COMMIT_AHEAD; ++j) younger += base + 64 * j < p_end;
+        retire_oldest(younger);
+        take((w + 1) & 3);
+        base += 64;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot w % 4's reads done
+        issue(base + 64 * COMMIT_AHEAD, (w + 1 + COMMIT_AHEAD) & 3);  // window w+1+AHEAD
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no untracked load outlives the walk
     if (lane == 0) {
@@ -522,23 +657,23 @@ bool commit_in_lds(int N) { return N <= LDS_CAP_MAX_NODES; }
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost, int32_t *halt, int batch,
-                         int32_t *pub) {
+                         int32_t *pub, const uint8_t *zrow) {
     if (p_begin >= 0 && p_end <= p_begin) return hipSuccess;
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
     if (Pp <= ONE_WAVE_MAX_PODS) {
         if (N <= LDS_CAP_MAX_NODES) {
-            const size_t lds = round_up(3 * (size_t)N * 4, 256);  // cap_to_lds pieces
+            const size_t lds = round_up(3 * (size_t)N * 4, 256) + PF_BYTES;  // cap_to_lds pieces + ring
             static std::atomic<unsigned long long> attr{0};
             hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit_w<true>),
                                         LDS_DYN_MAX, attr);
             if (e != hipSuccess) return e;
             k_commit_w<true><<<batch, 64, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
-                                                     out_node, oc, halt, nullptr);
+                                                     out_node, oc, halt, nullptr, zrow);
         } else {
-            k_commit_w<false><<<batch, 64, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
-                                                    out_node, oc, halt, pub);
+            k_commit_w<false><<<batch, 64, PF_BYTES, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
+                                                           out_node, oc, halt, pub, zrow);
         }
         return hipGetLastError();
     }
@@ -548,10 +683,10 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
         hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit<true>), LDS_DYN_MAX, attr);
         if (e != hipSuccess) return e;
         k_commit<true><<<batch, THREADS, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
-                                                oc, halt, nullptr);
+                                                oc, halt, nullptr, zrow);
     } else {
         k_commit<false><<<batch, THREADS, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
-                                               oc, halt, pub);
+                                               oc, halt, pub, zrow);
     }
     return hipGetLastError();
 }

@@ -41,7 +41,7 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int THREADS = 512;
+[[maybe_unused]] constexpr int THREADS = 512;  // the default (NWN = 4) workgroup, for tools/
 constexpr int BM = COST_BM;   // nodes per tile
 constexpr int BN = COST_BN;   // pods per tile
 constexpr int BKB = COST_BKB; // bytes of K per LDS stage (full 128-byte lines)

@@ -569,4 +569,32 @@ hipError_t launch_synth_overflow(hipStream_t st, uint64_t seed, int N, int P, in
     return hipGetLastError();
 }
 
+
+// zrow[r] = 1 iff row r of WA is all zero bytes and has no overflow entries:
+// one wave per row, 16 bytes per lane per load (row_bytes is a multiple of 128)
+__global__ void __launch_bounds__(256)
+k_zero_rows(const unsigned char *__restrict__ WA, int64_t rows, int64_t row_bytes,
+            const int32_t *__restrict__ ovf_ptr, uint8_t *__restrict__ zrow) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    const uint4 *p = reinterpret_cast<const uint4 *>(WA + r * row_bytes);
+    unsigned acc = 0;
+    for (int64_t i = lane; i < row_bytes / 16; i += 64) {
+        const uint4 v = p[i];
+        acc |= v.x | v.y | v.z | v.w;
+    }
+    const bool nz = __ballot(acc != 0) != 0;
+    if (lane == 0) zrow[r] = (!nz && (!ovf_ptr || ovf_ptr[r + 1] == ovf_ptr[r])) ? 1 : 0;
+}
+
+hipError_t launch_zero_rows(hipStream_t st, const void *WA, int64_t rows, int64_t row_bytes,
+                            const int32_t *ovf_ptr, uint8_t *zrow) {
+    if (rows <= 0) return hipSuccess;
+    if (row_bytes % 16) return hipErrorInvalidValue;
+    k_zero_rows<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(
+        static_cast<const unsigned char *>(WA), rows, row_bytes, ovf_ptr, zrow);
+    return hipGetLastError();
+}
+
 }  // namespace nas

@@ -278,6 +278,26 @@ int prepare_ovf(nas_ctx *ctx) {
     return NAS_OK;
 }
 
+// zero-traffic pods (k_commit.hip's scan past an exhausted list), once per
+// traffic upload, on the main stream like the other per-upload preparations
+int prepare_zrow(nas_ctx *ctx) {
+    if (ctx->zrow_valid) return NAS_OK;
+    const int64_t rows = (int64_t)ctx->B * ctx->Pp;
+    OK(nas::ensure(ctx, ctx->zrow, (size_t)rows));
+    HIPCK(nas::launch_zero_rows(ctx->stream, ctx->WA.p, rows, (int64_t)ctx->Kp * esz(ctx->dtype),
+                                ctx->ovf_n ? ctx->ovf_ptr.as<int32_t>() : nullptr,
+                                ctx->zrow.as<uint8_t>()));
+    ctx->zrow_valid = true;
+    return NAS_OK;
+}
+
+// the commit's zero-traffic flags, or nullptr when 0 x L may not be 0
+// (a float latency matrix holding Inf / NaN)
+const uint8_t *zrow_ptr(const nas_ctx *ctx) {
+    if (!ctx->zrow_valid || (ctx->dtype != NAS_DT_I8 && !ctx->L_finite)) return nullptr;
+    return ctx->zrow.as<uint8_t>();
+}
+
 // NAS_DT_F32 scores on the bf16 MFMA: both operands split into six K-segments
 // of bf16 planes (k_misc.hip k_split6), once per upload; every cost launch
 // then runs the bf16 kernel over K' = 6 Kp (launch_cost below)
@@ -500,7 +520,7 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t
     HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), ctx->Pp, -1, hi, ctx->cap.as<int32_t>(),
                              ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
-                             halt, 1, pub));
+                             halt, 1, pub, zrow_ptr(ctx)));
     tm.span(T_FIT, e1, e2);
     tm.span(T_COST, e2, e3);
     tm.span(T_MERGE, e3, e4);
@@ -555,7 +575,7 @@ int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi, int32_t *pub = nullptr) {
     HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), ctx->Pp, -1, hi, ctx->cap.as<int32_t>(),
                              ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
-                             halt, B, pub));
+                             halt, B, pub, zrow_ptr(ctx)));
     return NAS_OK;
 }
 
@@ -603,7 +623,8 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
     hipEvent_t e3 = tm.mark(st);
     HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), Pp, 0, P, ctx->cap.as<int32_t>(), N,
-                             ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt, B));
+                             ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt, B,
+                             nullptr, zrow_ptr(ctx)));
     tm.span(T_COMMIT, e3, tm.mark(st));
     int slots = 0;
     while (true) {
@@ -1180,6 +1201,18 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
         for (size_t i = 0, e = (size_t)ctx->B * n * n; i < e; ++i) mx = std::max(mx, std::abs((int)l[i]));
         ctx->L_abs_max = mx;
     }
+    // float latency: a zero-traffic pod's costs are exactly 0 only if no entry
+    // is Inf / NaN (the whole matrix: every rank decides the same)
+    ctx->L_finite = true;
+    if (dtype == NAS_DT_F32) {
+        const auto *l = static_cast<const uint32_t *>(L);
+        for (size_t i = 0, e = (size_t)ctx->B * n * n; i < e && ctx->L_finite; ++i)
+            ctx->L_finite = (l[i] & 0x7f800000u) != 0x7f800000u;
+    } else if (dtype == NAS_DT_BF16) {
+        const auto *l = static_cast<const uint16_t *>(L);
+        for (size_t i = 0, e = (size_t)ctx->B * n * n; i < e && ctx->L_finite; ++i)
+            ctx->L_finite = (l[i] & 0x7f80u) != 0x7f80u;
+    }
     if (ctx->have_wa && (ctx->wa_n != n || ctx->wa_dtype != dtype)) ctx->have_wa = false;
     const size_t e = esz(dtype);
     const size_t lt_b = (size_t)ctx->Mp * ctx->Kp * e;  // one cluster's Lt
@@ -1203,6 +1236,7 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n) {
     ctx->synth_valid = false;
     ctx->lr_valid = false;
     ctx->split_valid = false;
+    ctx->zrow_valid = false;
     ctx->scored = false;
     return NAS_OK;
 }
@@ -1305,6 +1339,7 @@ static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
     ctx->ovf_n = 0;
     ctx->wa_abs_row_max = 0;
     ctx->split_valid = false;
+    ctx->zrow_valid = false;
     ctx->scored = false;  // the lists (and their buffers' sizes) belong to the old inputs
     ctx->have_wa = false;
     return NAS_OK;
@@ -1548,6 +1583,7 @@ int nas_score(nas_ctx *ctx) {
     OK(alloc_extended(ctx));
     OK(prepare_ovf(ctx));
     OK(prepare_split(ctx));
+    OK(prepare_zrow(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     if (ctx->B > 1) OK(score_batch(ctx, tm));
@@ -1572,6 +1608,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     OK(alloc_extended(ctx));
     OK(prepare_ovf(ctx));
     OK(prepare_split(ctx));
+    OK(prepare_zrow(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     if (ctx->B > 1) return place_batch(ctx, tm, node_out, cost_out, int_score_out);
@@ -1666,7 +1703,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         HIPCK(nas::launch_commit(cs, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
-                                 1, pub));
+                                 1, pub, zrow_ptr(ctx)));
         tm.span(T_COMMIT, c0, tm.fine(cs));
         // this chunk's results go to the pinned stage right behind its
         // commit, and the host unpacks them while later chunks still run
@@ -1813,6 +1850,7 @@ int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi) {
     OK(alloc_extended(ctx));
     OK(prepare_ovf(ctx));
     OK(prepare_split(ctx));
+    OK(prepare_zrow(ctx));
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     OK(score_range(ctx, tm, p_lo, p_hi));
@@ -1887,6 +1925,7 @@ int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out
     if (!node_out || !stop_out || p_begin < 0 || p_begin > ctx->P)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_commit arguments");
     OK(alloc_extended(ctx));  // (scored implies they match; cheap when they do)
+    OK(prepare_zrow(ctx));
     const int P = ctx->P;
     *stop_out = P;
     if (p_begin == P) return NAS_OK;
@@ -1900,7 +1939,7 @@ int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out
     HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                              ctx->req.as<int32_t>(), ctx->Pp, p_begin, P, ctx->cap.as<int32_t>(),
                              ctx->N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
-                             halt));
+                             halt, 1, nullptr, zrow_ptr(ctx)));
     tm.span(T_COMMIT, c0, tm.mark(st));
     int32_t *hs = ctx->host_status.as<int32_t>();
     HIPCK(hipMemcpyAsync(hs, halt, 12, hipMemcpyDeviceToHost, st));
@@ -2104,6 +2143,8 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
     ctx->ovf_n = 0;
     ctx->lr_valid = false;
     ctx->split_valid = false;
+    ctx->zrow_valid = false;
+    ctx->L_finite = true;  // the synthetic latency classes are finite
     ctx->scored = false;
     if (dtype == NAS_DT_I8) {
         // exact traffic: peer aggregates beyond the int8 plane go to the

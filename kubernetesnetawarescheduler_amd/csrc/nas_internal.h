@@ -133,6 +133,11 @@ struct nas_ctx {
     int64_t wa_abs_row_max = 0; // max over pods of sum_m |WA[p,m]| (int8 path)
     int32_t L_abs_max = 0;      // max |L| (int8 path)
     bool scored = false;        // a scoring pass filled cand_key
+    // zero-traffic pods (k_commit.hip): zrow[B][Pp], valid for the uploaded
+    // traffic; L_finite: no Inf / NaN latency (float dtypes; 0 x Inf is not 0)
+    nas::DevBuf zrow;
+    bool zrow_valid = false;
+    bool L_finite = true;
     bool synth_valid = false;   // inputs came from nas_synth_cluster(synth_seed)
     uint64_t synth_seed = 0;
 
@@ -232,7 +237,11 @@ bool commit_in_lds(int N);
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost_i, int32_t *halt, int batch = 1,
-                         int32_t *pub = nullptr);
+                         int32_t *pub = nullptr, const uint8_t *zrow = nullptr);
+// zrow[r] = 1 iff traffic row r (row_bytes bytes of WA) is all zero bytes and
+// has no overflow entries (ovf_ptr may be null): the pod's every cost is 0
+hipError_t launch_zero_rows(hipStream_t st, const void *WA, int64_t rows, int64_t row_bytes,
+                            const int32_t *ovf_ptr, uint8_t *zrow);
 
 // gathered rescore (k_rescore.hip)
 int stale_words(int P);
