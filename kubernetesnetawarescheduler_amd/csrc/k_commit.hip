@@ -109,10 +109,15 @@ constexpr int ZSCAN_L2 = 16;
 // above its bound's node that fits the capacity read by `ld`.  Returns the
 // node, -1 when no node fits at all (the scan reached N), or -2 when the scan
 // limit ran out first (rescore).
+// `from` (per pod, -1 at first): where this pod's previous scan stopped -- the
+// nodes below it did not fit then and capacity only shrinks between picks
+// (a round's failed reservations are undone before the next round picks)
 template <bool LDS_CAP, typename LD>
-__device__ __forceinline__ int zero_row_scan(u64 bound, int r0, int r1, int r2, int N, LD &&ld) {
-    const int n0 = (int)(unsigned)bound + 1;
-    const int n1 = min(N, n0 + (LDS_CAP ? ZSCAN_LDS : ZSCAN_L2));
+__device__ __forceinline__ int zero_row_scan(u64 bound, int r0, int r1, int r2, int N, LD &&ld,
+                                             int &from) {
+    const int nb = (int)(unsigned)bound + 1;
+    const int n0 = max(nb, from);
+    const int n1 = min(N, nb + (LDS_CAP ? ZSCAN_LDS : ZSCAN_L2));
     // 8 nodes per step, their 24 reads in flight together (a node past n1
     // re-reads n1 - 1 and is never taken)
     for (int n = n0; n < n1; n += 8) {
@@ -123,8 +128,12 @@ __device__ __forceinline__ int zero_row_scan(u64 bound, int r0, int r1, int r2, 
             const int a = ld(m), b = ld(N + m), c = ld(2 * N + m);
             fit |= (unsigned)((r0 <= a) & (r1 <= b) & (r2 <= c) & (n + j < n1)) << j;
         }
-        if (fit) return n + __builtin_ctz(fit);
+        if (fit) {
+            from = n + __builtin_ctz(fit);
+            return from;
+        }
     }
+    from = n1;
     return n1 == N ? -1 : -2;
 }
 
@@ -284,6 +293,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         if (base + THREADS < p_end) load(base + THREADS, nxt);  // prefetch the next window
         const int i = base + tid;
         bool done = i >= p_end;
+        int zfrom = -1;  // zero-traffic scan resume point (zero_row_scan)
         while (true) {
             // slot (round + 1) % 3 was last read before the previous round's
             // first barrier and is next written after this round's: reset it
@@ -310,7 +320,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             if (done) choice = -1;
             bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
             if (COMMIT_ZSCAN && rescore && zrow && zrow[i] && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
-                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld);
+                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld, zfrom);
                 if (z != -2) {
                     rescore = false;
                     choice = z;  // -1: nothing fits (NAS_EMPTY)
@@ -537,30 +547,44 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     for (int base = p_begin, w = 0;; ++w) {
         const int i = base + lane;
         bool done = i >= p_end;
+        int zfrom = -1;  // zero-traffic scan resume point (zero_row_scan)
         while (true) {
             int choice = -1;
             unsigned ccost = 0;
             if (!done && COMMIT_BATCH) {
-                // every usable candidate's capacity at once (24 independent LDS
-                // reads, not up to 8 dependent rounds of 3): a herd member whose
-                // first candidates are full costs one LDS latency, not eight.
-                // Keys ascend and the unusable ones (> bound, KEY_INVALID) come
-                // last, so the lowest fitting bit is the sequential choice.
-                unsigned okm = 0;
-#pragma unroll
-                for (int j = 0; j < KC; ++j) {
-                    const u64 k = cur.k[j];
-                    const bool usable = k != KEY_INVALID && k <= cur.bound;
-                    const int n = usable ? (int)(unsigned)k : 0;
-                    const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
-                    okm |= (unsigned)(usable & (cur.r0 <= a) & (cur.r1 <= b) & (cur.r2 <= c)) << j;
-                }
-#pragma unroll
-                for (int j = KC - 1; j >= 0; --j)  // constant indices (no scratch array)
-                    if ((okm >> j) & 1u) {
-                        choice = (int)(unsigned)cur.k[j];
-                        ccost = (unsigned)(cur.k[j] >> 32);
+                // candidate 0 first: most pods take it (3 LDS reads)
+                const u64 k0 = cur.k[0];
+                bool more = k0 != KEY_INVALID && k0 <= cur.bound;
+                if (more) {
+                    const int n = (int)(unsigned)k0;
+                    if ((cur.r0 <= ld(n)) & (cur.r1 <= ld(N + n)) & (cur.r2 <= ld(2 * N + n))) {
+                        choice = n;
+                        ccost = (unsigned)(k0 >> 32);
+                        more = false;
                     }
+                }
+                // the rest at once for the pods whose first candidate is full
+                // (21 independent LDS reads, not up to 7 dependent rounds of
+                // 3): a herd member costs one LDS latency.  Keys ascend and the
+                // unusable ones (> bound, KEY_INVALID) come last, so the lowest
+                // fitting bit is the sequential choice.
+                if (__ballot(more) && more) {
+                    unsigned okm = 0;
+#pragma unroll
+                    for (int j = 1; j < KC; ++j) {
+                        const u64 k = cur.k[j];
+                        const bool usable = k != KEY_INVALID && k <= cur.bound;
+                        const int n = usable ? (int)(unsigned)k : 0;
+                        const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
+                        okm |= (unsigned)(usable & (cur.r0 <= a) & (cur.r1 <= b) & (cur.r2 <= c)) << j;
+                    }
+#pragma unroll
+                    for (int j = KC - 1; j >= 1; --j)  // constant indices (no scratch array)
+                        if ((okm >> j) & 1u) {
+                            choice = (int)(unsigned)cur.k[j];
+                            ccost = (unsigned)(cur.k[j] >> 32);
+                        }
+                }
             }
             if (!done && !COMMIT_BATCH) {
 #pragma unroll
@@ -577,7 +601,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             }
             bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
             if (COMMIT_ZSCAN && rescore && cur.z && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
-                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld);
+                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld, zfrom);
                 if (z != -2) {
                     rescore = false;
                     choice = z;  // -1: nothing fits (NAS_EMPTY)
