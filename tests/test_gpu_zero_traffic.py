@@ -176,3 +176,32 @@ def test_c2_needs_no_rescore():
     want, wcost, _ = oracle.place(WA, c["L"], c["req"], c["free"], "i8")
     assert node.tolist() == want.tolist() and score.tolist() == wcost.tolist()
     assert t["rescore_rounds"] == 0
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_zero_traffic_node_shards(G):
+    """Node shards (host exchange, replicated commit): every shard holds the
+    whole WA, so every shard flags the same zero-traffic pods and scans the
+    same replicated capacity -- equal to the oracle and on every shard."""
+    from kubernetesnetawarescheduler_amd.sharded import place_local_shards
+    P, N = 3000, 400
+    rng = np.random.default_rng(11 + G)
+    WA, L, free, req = cluster(rng, P, N, lo=0, hi=40, cap_scale=0.05)
+    WA[rng.random(P) < 0.5] = 0
+    engines = []
+    try:
+        for r in range(G):
+            e = Engine(0)
+            engines.append(e)
+            e.set_shard(r, G)
+            upload(e, WA, L, free, req)
+        node, score, _ = place_local_shards(engines, P)
+        caps = [e.get_capacity() for e in engines]
+    finally:
+        for e in engines:
+            e.close()
+    want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+    assert node.tolist() == want.tolist()
+    assert score.tolist() == wcost.tolist()
+    for c in caps:
+        assert (c == wfree).all()
