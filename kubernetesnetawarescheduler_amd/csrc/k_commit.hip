@@ -83,10 +83,13 @@ __device__ __forceinline__ void retire_oldest(int younger);
 constexpr int LDS_CAP_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 12;  // + cap_to_lds padding
 constexpr int NO_POD = 0x7fffffff;
 // walks of up to this many pods run in one wave (k_commit_w): fewer, exact
-// stops for herds on small clusters (C2: 0.67 -> 0.62 ms per pass); longer
+// stops for herds on small clusters (C2: 0.67 -> 0.62 ms per pass; with the
+// zero-traffic scan and no rescore left, 0.55 vs 0.63 ms for k_commit); longer
 // walks keep the 1024-pod windows of k_commit, whose conflict-free rounds
 // commit 16x more pods each (C3: 0.8 vs 2.4 ms of commit per pass)
-constexpr int ONE_WAVE_MAX_PODS = 16384;
+#ifndef ONE_WAVE_MAX_PODS
+#define ONE_WAVE_MAX_PODS 16384
+#endif
 
 // Requests up to this size reserve with one fetch-and-subtract (undone on
 // failure) instead of a compare-and-swap loop: a herd of m pods picking one
@@ -557,7 +560,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 bool more = k0 != KEY_INVALID && k0 <= cur.bound;
                 if (more) {
                     const int n = (int)(unsigned)k0;
-                    if ((cur.r0 <= ld(n)) & (cur.r1 <= ld(N + n)) & (cur.r2 <= ld(2 * N + n))) {
+                    if ((int)(cur.r0 <= ld(n)) & (int)(cur.r1 <= ld(N + n)) & (int)(cur.r2 <= ld(2 * N + n))) {
                         choice = n;
                         ccost = (unsigned)(k0 >> 32);
                         more = false;
