@@ -58,8 +58,9 @@ constexpr int THREADS = 1024;  // one window of pods per round
 constexpr int LDS_DYN_MAX = 160 * 1024 - 512;  // leaves room for the static LDS
 // k_commit_w's prefetch ring of candidate lists in LDS (after the capacity):
 // PF_SLOTS windows of 64 pods, PF_SLOT bytes each -- keys [64][8] u64 at 0,
-// bounds [64] u64 at 4096 (+512 written by the idle half of the wave), requests
-// [3][64] int32 at 5120, zero-traffic flags [64] bytes at 5888 (+192 idle)
+// bounds [128] u64 from the even pod at or below the window at 4096, requests
+// [3][64] int32 at 5120, zero-traffic flags [256] bytes from the multiple of 4
+// at or below the window at 5888
 constexpr int PF_SLOT = 6144;
 constexpr int PF_SLOTS = 4;
 constexpr int PF_BYTES = PF_SLOT * PF_SLOTS;
@@ -521,21 +522,24 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             glds<16>(kb + min((size_t)wbase * KC * 8 + j * 1024 + lane * 16, kmax), d + j * 1024);
+        // bounds and flags from aligned starts (a window may begin at any pod
+        // after a halt): 16-byte pieces from the even pod below, dwords from
+        // the multiple of 4 below; take() skips the leading entries
         glds<16>(reinterpret_cast<const unsigned char *>(cand_bound) +
-                     min((size_t)wbase * 8 + lane * 16, (size_t)Pp * 8 - 16),
+                     min((size_t)(wbase & ~1) * 8 + lane * 16, (size_t)Pp * 8 - 16),
                  d + 4096);
 #pragma unroll
         for (int r = 0; r < 3; ++r) glds<4>(req + (size_t)r * Pp + min(wbase + lane, Pp - 1), d + 5120 + r * 256);
-        glds<4>(zsrc + min(wbase + 4 * lane, Pp - 4), d + 5888);
+        glds<4>(zsrc + min((wbase & ~3) + 4 * lane, Pp - 4), d + 5888);
     };
-    auto take = [&](int slot) {
+    auto take = [&](int slot, int wbase) {
         const unsigned char *d = pf + slot * PF_SLOT;
         load8(reinterpret_cast<const u64 *>(d) + lane * KC, cur.k);
-        cur.bound = reinterpret_cast<const u64 *>(d + 4096)[lane];
+        cur.bound = reinterpret_cast<const u64 *>(d + 4096)[lane + (wbase & 1)];
         cur.r0 = reinterpret_cast<const int *>(d + 5120)[lane];
         cur.r1 = reinterpret_cast<const int *>(d + 5120 + 256)[lane];
         cur.r2 = reinterpret_cast<const int *>(d + 5120 + 512)[lane];
-        cur.z = zrow ? (int)d[5888 + lane] : 0;
+        cur.z = zrow ? (int)d[5888 + lane + (wbase & 3)] : 0;
     };
     // windows 0..3 into slots 0..3; window w always sits in slot w % 4
     int younger = 0;
@@ -544,7 +548,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         younger += j > 0 && p_begin + 64 * j < p_end;
     }
     retire_oldest(younger);
-    take(0);
+    take(0, p_begin);
     int round = 0;
     int stop = p_end;
     for (int base = p_begin, w = 0;; ++w) {
@@ -663,7 +667,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         younger = 0;
         for (int j = 2; j <= COMMIT_AHEAD; ++j) younger += base + 64 * j < p_end;
         retire_oldest(younger);
-        take((w + 1) & 3);
+        take((w + 1) & 3, base + 64);
         base += 64;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot w % 4's reads done
         issue(base + 64 * COMMIT_AHEAD, (w + 1 + COMMIT_AHEAD) & 3);  // window w+1+AHEAD
