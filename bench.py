@@ -185,6 +185,31 @@ class Dist:
         return obj[0]
 
 
+def agree(d, ok):
+    """True only if `ok` holds on every rank (gloo MIN); every rank must call."""
+    if d.world == 1:
+        return ok
+    t = d.torch.tensor([1 if ok else 0], dtype=d.torch.int64)
+    d.dist.all_reduce(t, op=d.dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
+def host_all_gather(d):
+    """sharded.place_dist_shard's exchange over the gloo process group: every
+    rank's (keys, bounds) in rank order."""
+    torch = d.torch
+
+    def ag(keys, bounds):
+        k = torch.from_numpy(np.ascontiguousarray(keys).view(np.int64))
+        b = torch.from_numpy(np.ascontiguousarray(bounds).view(np.int64))
+        ks = [torch.empty_like(k) for _ in range(d.world)]
+        bs = [torch.empty_like(b) for _ in range(d.world)]
+        d.dist.all_gather(ks, k)
+        d.dist.all_gather(bs, b)
+        return [(x.numpy().view(np.uint64), y.numpy().view(np.uint64)) for x, y in zip(ks, bs)]
+    return ag
+
+
 def time_steps(d, fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -197,20 +222,49 @@ def time_steps(d, fn, steps, warmup):
 
 
 def bench_place(args, d, eng):
+    """Returns (elapsed, per-stage times, placements, the engine to use from
+    here on, how the node shards exchange their lists)."""
     N, P = args.nodes, args.pods
     if args.rehearse_world > 1:
         assert d.world == 1, "--rehearse-world runs on one GPU"
         eng.set_option("REHEARSE_WORLD", args.rehearse_world)  # diagnostic option
+    exchange = None
     if d.world > 1 or args.rccl_world1 or args.rehearse_world > 1:
-        uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
-        eng.comm_init(uid, d.rank, d.world)
-    eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
-    if args.rehearse_world > 1:
-        # the stand-in lists repeat this rank's few best nodes G times, so
-        # herds would drain them at once; with 64x capacity no list runs dry
-        # and the pass times scoring + exchange + merge + the full commit walk
-        eng.upload_capacity(np.minimum(eng.get_capacity().astype(np.int64) * 64,
-                                       2**31 - 1).astype(np.int32))
+        exchange = "rccl all-gather (nas_comm_init)"
+        err = None
+        try:
+            eng.set_option("COMM_TIMEOUT_MS", 60000)
+            uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
+            eng.comm_init(uid, d.rank, d.world)
+            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+            if args.rehearse_world > 1:
+                # the stand-in lists repeat this rank's few best nodes G times,
+                # so herds would drain them at once; with 64x capacity no list
+                # runs dry and the pass times scoring + exchange + merge + the
+                # full commit walk
+                eng.upload_capacity(np.minimum(eng.get_capacity().astype(np.int64) * 64,
+                                               2**31 - 1).astype(np.int32))
+            eng.reset_capacity()
+            eng.place()  # first collectives (connection setup) inside the deadline
+        except Exception as e:  # noqa: BLE001 -- decided together below
+            err = repr(e)[:300]
+        if not agree(d, err is None):
+            if d.world == 1:
+                raise RuntimeError(f"RCCL path failed: {err}")
+            # RCCL unusable on this node: the same kernels on the same node
+            # shards, candidate lists exchanged through the host over gloo
+            # (sharded.place_dist_shard) -- slower, reported as such
+            print(f"rank {d.rank}: RCCL path failed ({err or 'on another rank'}); "
+                  "host exchange over gloo", file=sys.stderr, flush=True)
+            eng.close()
+            from kubernetesnetawarescheduler_amd import Engine
+            eng = Engine(d.local)
+            eng.set_shard(d.rank, d.world)
+            exchange = f"host gloo all-gather (RCCL failed: {err or 'on another rank'})"
+            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+            return bench_place_host(args, d, eng) + (eng, exchange)
+    else:
+        eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
     keys = ("cost_ms", "fit_ms", "merge_ms", "commit_ms", "total_ms", "cost_launches",
             "rescore_rounds", "unschedulable")
     acc = dict.fromkeys(keys, 0.0)
@@ -243,6 +297,27 @@ def bench_place(args, d, eng):
         step()
     per.update({k: acc[k] / n_stage for k in ("cost_ms", "fit_ms", "merge_ms", "commit_ms",
                                                 "total_ms")})
+    return elapsed, per, state["node"], eng, exchange
+
+
+def bench_place_host(args, d, eng):
+    """The placement pass with the node shards' lists exchanged through the
+    host (fallback when RCCL is unusable): score, gloo all-gather, merge,
+    replicated commit, rescore windows -- sharded.place_dist_shard."""
+    from kubernetesnetawarescheduler_amd import sharded
+    P = args.pods
+    ag = host_all_gather(d)
+    state = {"node": None, "rounds": 0}
+
+    def step():
+        eng.reset_capacity()
+        node, _, rounds = sharded.place_dist_shard(eng, P, ag)
+        state["node"], state["rounds"] = node, rounds
+
+    elapsed = time_steps(d, step, args.steps, args.warmup)
+    per = {"cost_ms": 0.0, "fit_ms": 0.0, "merge_ms": 0.0, "commit_ms": 0.0, "total_ms": 0.0,
+           "rescore_rounds": float(state["rounds"]),
+           "unschedulable": float((state["node"] < 0).sum())}
     return elapsed, per, state["node"]
 
 
@@ -751,7 +826,9 @@ def main():
                             "its node columns scored, the other ranks' lists stood in for by "
                             "shifted copies; NOT a multi-GPU measurement, placements not checked")
     if args.only not in ("vote", "score", "pmc"):
-        elapsed, per, gpu_nodes = bench_place(args, d, eng)
+        elapsed, per, gpu_nodes, eng, exchange = bench_place(args, d, eng)
+        if exchange:
+            out["config"]["exchange"] = exchange
         out["value"] = P * N / (elapsed / args.steps)
         out["ms_per_step"] = elapsed * 1e3 / args.steps
         out["placements_per_s"] = P / (elapsed / args.steps)
