@@ -389,6 +389,75 @@ def vendor_gemm_reference(args, d, reps=5):
         torch.cuda.empty_cache()
 
 
+def bench_host(args):
+    """SURVEY.md §8(f) next-1 / next-2 on the host (libnas_host.so, no GPU):
+    a snapshot refresh -- every node's node-exporter text parsed with the
+    reference's Go semantics (scheduler.go:275-331, :396-549) into the SoA
+    arrays nas_upload_snapshot takes, one thread and the host's share of
+    threads -- and the pairwise latency matrix from all-pairs iperf3 reports
+    (scheduler.go:503-530 per pair).  The reference parses 5 scraped bodies
+    per pod, sequentially, inside its scheduling loop."""
+    import ctypes as C
+    from kubernetesnetawarescheduler_amd import hostlib as H
+    from kubernetesnetawarescheduler_amd.exporter_text import exporter_body, iperf_report
+    rng = np.random.default_rng(SEED)
+    n = args.nodes
+    names = [f"raspiworker{i}" for i in range(n)]
+    bodies = [exporter_body(names[i], rng.choice([6e8, 1.2e9, 1.5e9, 1.8e9], 4),
+                            float(rng.integers(5e8, 9e9)), float(rng.integers(1e8, 5e8)),
+                            int(rng.integers(0, 3e6)), int(rng.integers(0, 3e6)),
+                            int(rng.integers(0, 9))).encode() for i in range(n)]
+    nbytes = sum(len(b) for b in bodies)
+    arr = (C.c_char_p * n)(*bodies)
+    lens = (C.c_size_t * n)(*[len(b) for b in bodies])
+    nm = (C.c_char_p * n)(*[x.encode() for x in names])
+    outs = [np.zeros(n, np.float64), np.zeros(n, np.float64)] + [np.zeros(n, np.int64) for _ in range(3)]
+    status = np.zeros(n, np.int32)
+    ptrs = [o.ctypes.data_as(C.c_void_p) for o in outs] + [status.ctypes.data_as(C.c_void_p)]
+    cores = cpu_info()
+    threads = cores["omp_num_threads"] or min(16, cores["usable"] or 1)
+
+    def run(t, reps=5):
+        ms = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            rc = H.hostlib().nas_host_snapshot_from_bodies(n, arr, lens, nm, *ptrs, t)
+            ms.append((time.perf_counter() - t0) * 1e3)
+            assert rc == 0
+        return float(np.median(ms)), [o.copy() for o in outs]
+
+    ms1, r1 = run(1)
+    msT, rT = run(threads)
+    same = all(np.array_equal(a, b) for a, b in zip(r1, rT)) and not status.any()
+    # spot-check against the one-node entry point (the ingest tests pin it)
+    spot = all(H.node_metrics(bodies[i], names[i]) ==
+               (r1[0][i], r1[1][i], int(r1[2][i]), int(r1[3][i]), int(r1[4][i]))
+               for i in range(0, n, max(1, n // 64)))
+    g = 100
+    reps = [[None if i == j else iperf_report(float(rng.uniform(2e8, 9.4e8))).encode()
+             for j in range(g)] for i in range(g)]
+    flat = [reps[i][j] for i in range(g) for j in range(g)]
+    rarr = (C.c_char_p * (g * g))(*flat)
+    rlen = (C.c_size_t * (g * g))(*[0 if x is None else len(x) for x in flat])
+    L = np.zeros((g, g), np.float32)
+    lm = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        assert H.hostlib().nas_host_latency_matrix_us(g, rarr, rlen, L.ctypes.data_as(C.c_void_p)) == 0
+        lm.append((time.perf_counter() - t0) * 1e3)
+    lm_ms = float(np.median(lm))
+    return {"snapshot_ingest": {"nodes": n, "bytes": nbytes, "ms_1_thread": ms1,
+                                "nodes_per_s_1_thread": n / (ms1 * 1e-3), "threads": threads,
+                                "ms": msT, "nodes_per_s": n / (msT * 1e-3),
+                                "MB_per_s": nbytes / (msT * 1e-3) / 1e6,
+                                "thread_count_free": same, "matches_node_metrics": spot},
+            "latency_matrix_us": {"nodes": g, "reports": g * (g - 1), "ms": lm_ms,
+                                  "reports_per_s": g * (g - 1) / (lm_ms * 1e-3)},
+            "cpu": cores,
+            "note": "host mirror (libnas_host.so), CPU only; synthetic node-exporter 0.18 "
+                    "bodies and iperf3 -J reports (exporter_text.py)"}
+
+
 def bench_vote(args, d, eng):
     N = args.nodes
     if args.vote_node_shard:
@@ -898,6 +967,8 @@ def main():
     eng.close()
     if d.world == 1 and not args.no_configs and args.only is None:
         out["configs"] = run_configs(args, d)
+    if d.rank == 0 and d.world == 1 and args.only is None and not args.no_configs:
+        out["host"] = bench_host(args)
     if args.c4 and "C4" not in out.get("configs", {}):
         from kubernetesnetawarescheduler_amd import Engine
         with Engine(d.local) as e:

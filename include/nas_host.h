@@ -50,6 +50,19 @@ int nas_host_node_metrics(const char *body, size_t n, const char *node, double *
                           int64_t *rx, int64_t *tx, int64_t *disk, char *panic_msg,
                           size_t panic_cap);
 
+/* A snapshot refresh: node i's node-exporter text bodies[i] (body_len[i]
+ * bytes) under name names[i], each as nas_host_node_metrics, into SoA
+ * arrays ready for nas_upload_snapshot (bandwidth comes from the iperf
+ * reports, so the caller fills it).  status[i] = NAS_OK or NAS_HOST_PANIC
+ * (that node's values are then 0: the reference would have crashed).  The
+ * nodes are split over `threads` worker threads (<= 0: the hardware's
+ * concurrency); the results do not depend on the thread count.  Replaces the
+ * reference's per-pod sequential scrape-and-parse of :275-331 with one
+ * parallel parse per refresh. */
+int nas_host_snapshot_from_bodies(int32_t n, const char *const *bodies, const size_t *body_len,
+                                  const char *const *names, double *cpu, double *mem, int64_t *rx,
+                                  int64_t *tx, int64_t *disk, int32_t *status, int32_t threads);
+
 /* json.Unmarshal into Iperf (:34-117, :551-555) and End.Streams[0]
  * (:525-528).  *n_streams == 0 is where the reference panics (index out of
  * range); *valid_json == 0 means Unmarshal rejected the document. */

@@ -1,8 +1,10 @@
 // capi.cpp -- extern "C" surface of the host mirror (include/nas_host.h):
 // adapts the callback table to the C++ interfaces of scheduler.h and keeps
 // every exception on this side of the ABI.
+#include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "go_json.h"
@@ -163,6 +165,47 @@ int nas_host_node_metrics(const char *body, size_t n, const char *node, double *
         copy_str(panic_msg, panic_cap, e.what());
         return NAS_HOST_PANIC;
     }
+    return NAS_OK;
+}
+
+int nas_host_snapshot_from_bodies(int32_t n, const char *const *bodies, const size_t *body_len,
+                                  const char *const *names, double *cpu, double *mem, int64_t *rx,
+                                  int64_t *tx, int64_t *disk, int32_t *status, int32_t threads) {
+    if (n < 0 || (n > 0 && (!bodies || !body_len || !names || !cpu || !mem || !rx || !tx ||
+                            !disk || !status)))
+        return NAS_ERR_ARG;
+    for (int32_t i = 0; i < n; ++i)
+        if ((!bodies[i] && body_len[i]) || !names[i]) return NAS_ERR_ARG;
+    auto one = [&](int32_t i) {
+        const std::string_view b(bodies[i] ? bodies[i] : "", body_len[i]);
+        try {
+            const double c = get_current_cpu_usage(b);
+            const double m = get_occupied_memory_percentage(b);
+            const int64_t r = get_network_packets_received(b, names[i]);
+            const int64_t t = get_network_packets_sent(b, names[i]);
+            const int64_t d = get_disk_io_now(b, names[i]);
+            cpu[i] = c, mem[i] = m, rx[i] = r, tx[i] = t, disk[i] = d;
+            status[i] = NAS_OK;
+        } catch (const GoPanic &) {
+            cpu[i] = mem[i] = 0;
+            rx[i] = tx[i] = disk[i] = 0;
+            status[i] = NAS_HOST_PANIC;
+        }
+    };
+    int w = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    w = std::max(1, std::min<int>(w, n / 64 + 1));  // >= 64 nodes per worker
+    if (w == 1) {
+        for (int32_t i = 0; i < n; ++i) one(i);
+        return NAS_OK;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve(w);
+    for (int k = 0; k < w; ++k)
+        pool.emplace_back([&, k] {
+            const int32_t lo = (int32_t)((int64_t)n * k / w), hi = (int32_t)((int64_t)n * (k + 1) / w);
+            for (int32_t i = lo; i < hi; ++i) one(i);
+        });
+    for (auto &t : pool) t.join();
     return NAS_OK;
 }
 

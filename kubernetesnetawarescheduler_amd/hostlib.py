@@ -63,6 +63,10 @@ SIGNATURES = {
     "nas_host_node_metrics": (_c.c_int, [_c.c_char_p, _c.c_size_t, _c.c_char_p, _F64P, _F64P,
                                          _I64P, _I64P, _I64P, _c.c_char_p, _c.c_size_t]),
     "nas_host_iperf_receiver": (_c.c_int, [_c.c_char_p, _c.c_size_t, _F64P, _F64P, _I32P, _I32P]),
+    "nas_host_snapshot_from_bodies": (_c.c_int, [_c.c_int32, _c.POINTER(_c.c_char_p),
+                                                 _c.POINTER(_c.c_size_t), _c.POINTER(_c.c_char_p),
+                                                 _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                                 _c.c_void_p, _c.c_void_p, _c.c_void_p, _c.c_int32]),
     "nas_host_latency_matrix": (_c.c_int, [_c.c_int32, _c.POINTER(_c.c_char_p),
                                            _c.POINTER(_c.c_size_t), _c.c_void_p]),
     "nas_host_latency_from_bps": (_c.c_int32, [_c.c_double]),
@@ -131,6 +135,25 @@ def node_metrics(body, node):
     if rc == NAS_HOST_PANIC:
         raise GoPanicError(msg.value.decode())
     return cpu.value, mem.value, rx.value, tx.value, disk.value
+
+
+def snapshot_from_bodies(bodies, names, threads=1):
+    """n node-exporter bodies -> dict of SoA arrays (cpu, mem, rx, tx, disk)
+    and status (0 or NAS_HOST_PANIC per node), parsed by `threads` workers."""
+    n = len(bodies)
+    bs = [_b(x) for x in bodies]
+    arr = (_c.c_char_p * n)(*bs)
+    lens = (_c.c_size_t * n)(*[len(x) for x in bs])
+    nm = (_c.c_char_p * n)(*[_b(x) for x in names])
+    out = {k: np.zeros(n, np.float64) for k in ("cpu", "mem")}
+    out.update({k: np.zeros(n, np.int64) for k in ("rx", "tx", "disk")})
+    out["status"] = np.zeros(n, np.int32)
+    rc = hostlib().nas_host_snapshot_from_bodies(
+        n, arr, lens, nm, *[out[k].ctypes.data_as(_c.c_void_p)
+                            for k in ("cpu", "mem", "rx", "tx", "disk", "status")], threads)
+    if rc != 0:
+        raise NasError(rc, "nas_host_snapshot_from_bodies")
+    return out
 
 
 def iperf_receiver(data):

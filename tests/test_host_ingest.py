@@ -260,3 +260,35 @@ def test_host_abi_symbols():
     for name in declared:
         assert hasattr(L, name)
     json.dumps(sorted(declared))
+
+
+# ------------------------------------------- snapshot refresh (batch ingest)
+def test_snapshot_from_bodies_equals_per_node_and_thread_count_free():
+    """nas_host_snapshot_from_bodies: every node equal to nas_host_node_metrics
+    on its own (a panicking node reports NAS_HOST_PANIC and zeros), for 1, 3
+    and 16 worker threads."""
+    rng = np.random.default_rng(3)
+    names, bodies = [], []
+    for i in range(700):
+        name = "ubuntu" if i % 97 == 0 else f"raspiworker{i}"
+        body = exporter_body(name, rng.choice([6e8, 1.2e9, 1.5e9, 1.8e9], 4),
+                             float(rng.integers(5e8, 9e9)), float(rng.integers(1e8, 5e8)),
+                             int(rng.integers(0, 3e6)), int(rng.integers(0, 3e6)),
+                             int(rng.integers(0, 9)))
+        if i % 113 == 5:
+            body = body.replace("node_disk_io_now", "node_disk_io_later")  # marker missing: panic
+        names.append(name)
+        bodies.append(body)
+    want = []
+    for b, n in zip(bodies, names):
+        try:
+            want.append((0,) + H.node_metrics(b, n))
+        except H.GoPanicError:
+            want.append((H.NAS_HOST_PANIC, 0.0, 0.0, 0, 0, 0))
+    assert any(w[0] == H.NAS_HOST_PANIC for w in want)
+    for threads in (1, 3, 16):
+        got = H.snapshot_from_bodies(bodies, names, threads)
+        for i, w in enumerate(want):
+            g = (int(got["status"][i]), got["cpu"][i], got["mem"][i], int(got["rx"][i]),
+                 int(got["tx"][i]), int(got["disk"][i]))
+            assert g == w, (threads, i)
