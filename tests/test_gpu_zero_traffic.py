@@ -90,7 +90,7 @@ def test_zero_traffic_scan_limit_falls_back_to_rescore(engine):
 
 
 def test_zero_traffic_l2_commit(engine):
-    """N > 13,653: the capacity lives in L2 (short scans, rescore beyond)."""
+    """N > 11,541: the capacity lives in L2 (short scans, rescore beyond)."""
     P, N = 17000, 14000  # > 16,384 pods: the 1024-thread commit, capacity in L2
     rng = np.random.default_rng(7)
     req = np.stack([rng.integers(1, 540, P), rng.integers(7_464, 303_749, P),
