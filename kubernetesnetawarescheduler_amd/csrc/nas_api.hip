@@ -626,6 +626,22 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
                              ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt, B,
                              nullptr, zrow_ptr(ctx)));
     tm.span(T_COMMIT, e3, tm.mark(st));
+    // every cluster's placements (and raw scores) go to the pinned stage right
+    // behind the commit, before the status words: when no cluster stopped,
+    // the one status round trip brings the results with it
+    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
+    const size_t BP = (size_t)B * P;
+    const bool want_raw = cost_out || int_score_out;
+    auto fetch = [&]() -> int {
+        HIPCK(hipMemcpy2DAsync(stage, (size_t)P * 4, ctx->out_node.p, (size_t)Pp * 4,
+                               (size_t)P * 4, B, hipMemcpyDeviceToHost, st));
+        if (want_raw)
+            HIPCK(hipMemcpy2DAsync(stage + BP, (size_t)P * 4, ctx->out_cost_i.p, (size_t)Pp * 4,
+                                   (size_t)P * 4, B, hipMemcpyDeviceToHost, st));
+        return NAS_OK;
+    };
+    OK(fetch());
+    hipEvent_t t1 = tm.mark(st);
     int slots = 0;
     while (true) {
         HIPCK(hipMemcpyAsync(hs, halt, (size_t)B * nas::STATUS_INTS * 4, hipMemcpyDeviceToHost, st));
@@ -643,33 +659,34 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
         tm.span(T_COMMIT, c0, tm.mark(st));
         ctx->timings.cost_launches += 1;
     }
-    std::vector<uint32_t> raw;
-    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
-    const size_t BP = (size_t)B * P;
-    HIPCK(hipMemcpy2DAsync(stage, (size_t)P * 4, ctx->out_node.p, (size_t)Pp * 4, (size_t)P * 4,
-                           B, hipMemcpyDeviceToHost, st));
-    if (cost_out || int_score_out) {
-        raw.resize(BP);
-        HIPCK(hipMemcpy2DAsync(stage + BP, (size_t)P * 4, ctx->out_cost_i.p, (size_t)Pp * 4,
-                               (size_t)P * 4, B, hipMemcpyDeviceToHost, st));
+    if (slots > 0) {  // the walk moved on after the speculative copies
+        OK(fetch());
+        t1 = tm.mark(st);
+        HIPCK(hipStreamSynchronize(st));
     }
-    hipEvent_t t1 = tm.mark(st);
-    HIPCK(hipStreamSynchronize(st));
-    std::memcpy(node_out, stage, BP * 4);
-    if (!raw.empty()) std::memcpy(raw.data(), stage + BP, BP * 4);
     tm.span(T_TOTAL, t0, t1);
+    std::memcpy(node_out, stage, BP * 4);
+    const uint32_t *raw = reinterpret_cast<const uint32_t *>(stage + BP);
     int unsched = 0, dev_rounds = 0, rounds = 0;
     for (int b = 0; b < B; ++b) {
         dev_rounds += hs[b * nas::STATUS_INTS + 1];
         rounds += hs[b * nas::STATUS_INTS + 2];
     }
-    for (size_t i = 0; i < (size_t)B * P; ++i) {
-        const bool none = node_out[i] < 0;
-        unsched += none;
-        if (cost_out) cost_out[i] = none ? 0.f : decode_cost(raw[i], ctx->dtype);
-        if (int_score_out)
-            int_score_out[i] = (none || ctx->dtype != NAS_DT_I8)
-                                   ? 0 : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
+    // branch-free per-pod loops (they vectorise): 320k pods at C5
+    for (size_t i = 0; i < BP; ++i) unsched += node_out[i] < 0;
+    if (cost_out) {
+        if (ctx->dtype == NAS_DT_I8) {
+            for (size_t i = 0; i < BP; ++i)
+                cost_out[i] = node_out[i] < 0 ? 0.f : (float)(int32_t)(raw[i] ^ 0x80000000u);
+        } else {
+            for (size_t i = 0; i < BP; ++i)
+                cost_out[i] = node_out[i] < 0 ? 0.f : decode_cost(raw[i], ctx->dtype);
+        }
+    }
+    if (int_score_out) {
+        const bool i8 = ctx->dtype == NAS_DT_I8;
+        for (size_t i = 0; i < BP; ++i)
+            int_score_out[i] = (node_out[i] < 0 || !i8) ? 0 : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
     }
     ctx->timings.fit_ms = tm.total(T_FIT);
     ctx->timings.cost_ms = tm.total(T_COST);
