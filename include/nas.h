@@ -93,7 +93,9 @@ typedef struct nas_config {
                                    * On expiry the communicators are aborted
                                    * (ncclCommAbort), the call returns NAS_ERR_COMM and the
                                    * context is poisoned: every later call except
-                                   * nas_last_error / nas_destroy returns NAS_ERR_COMM */
+                                   * nas_last_error / nas_destroy returns NAS_ERR_COMM.
+                                   * It also bounds nas_comm_init: communicators not built
+                                   * by then (a rank never joined) -> NAS_ERR_COMM */
 #define NAS_OPT_REHEARSE_WORLD 3 /* DIAGNOSTIC, default 0.  G > 1, set before nas_comm_init
                                   * with world 1: the context takes rank 0's shard geometry
                                   * of a G-rank node shard and stands the other ranks' lists

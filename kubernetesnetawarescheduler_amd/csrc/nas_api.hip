@@ -9,7 +9,10 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -2017,21 +2020,66 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     }
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
-    ncclComm_t comm, comm2 = nullptr, comm_c = nullptr;
-    ncclResult_t r = ncclCommInitRank(&comm, world, uid, rank);
-    if (r != ncclSuccess)
-        return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-    ctx->comm = reinterpret_cast<ncclComm *>(comm);
-    // one communicator per stream that issues collectives (second scoring
-    // stream, commit stream): each keeps its own issue order on every rank
-    r = ncclCommSplit(comm, 0, rank, &comm2, nullptr);
-    if (r == ncclSuccess) r = ncclCommSplit(comm, 0, rank, &comm_c, nullptr);
-    ctx->comm2 = reinterpret_cast<ncclComm *>(comm2);
-    ctx->comm_c = reinterpret_cast<ncclComm *>(comm_c);
-    if (r != ncclSuccess) {
-        destroy_comms(ctx);
-        return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclCommSplit: ") + ncclGetErrorString(r));
+    // The communicators are built on a helper thread under the context's
+    // NAS_OPT_COMM_TIMEOUT_MS deadline: ncclCommInitRank and ncclCommSplit
+    // block until every rank has joined, so a rank whose peers never arrive
+    // (a failed launch, an unreachable bootstrap address) would otherwise hang
+    // here with no way out.  On expiry the call returns NAS_ERR_COMM and the
+    // helper is abandoned; should it still finish, it destroys what it built.
+    // (Blocking communicators are kept: non-blocking ones would make every
+    // collective of the pass return ncclInProgress.)
+    struct Init {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool done = false, abandoned = false;
+        ncclResult_t r = ncclSuccess;
+        const char *what = "";
+        ncclComm_t comm = nullptr, comm2 = nullptr, comm_c = nullptr;
+    };
+    auto st = std::make_shared<Init>();
+    const int dev = ctx->device;
+    std::thread([st, dev, uid, rank, world]() mutable {
+        ncclComm_t c = nullptr, c2 = nullptr, cc = nullptr;
+        const char *what = "ncclCommInitRank";
+        ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
+        if (r == ncclSuccess) r = ncclCommInitRank(&c, world, uid, rank);
+        // one communicator per stream that issues collectives (second scoring
+        // stream, commit stream): each keeps its own issue order on every rank
+        if (r == ncclSuccess) {
+            what = "ncclCommSplit";
+            r = ncclCommSplit(c, 0, rank, &c2, nullptr);
+            if (r == ncclSuccess) r = ncclCommSplit(c, 0, rank, &cc, nullptr);
+        }
+        std::lock_guard<std::mutex> g(st->mu);
+        if (st->abandoned || r != ncclSuccess) {  // abort: local, no peer handshake
+            for (ncclComm_t x : {cc, c2, c})
+                if (x) (void)ncclCommAbort(x);
+            c = c2 = cc = nullptr;
+        }
+        st->r = r;
+        st->what = what;
+        st->comm = c, st->comm2 = c2, st->comm_c = cc;
+        st->done = true;
+        st->cv.notify_all();
+    }).detach();
+    std::unique_lock<std::mutex> lk(st->mu);
+    if (ctx->opt_comm_timeout_ms > 0) {
+        if (!st->cv.wait_for(lk, std::chrono::milliseconds(ctx->opt_comm_timeout_ms),
+                             [&] { return st->done; })) {
+            st->abandoned = true;
+            return nas::fail(ctx, NAS_ERR_COMM,
+                             "nas_comm_init: the communicators were not built within " +
+                                 std::to_string(ctx->opt_comm_timeout_ms) +
+                                 " ms (NAS_OPT_COMM_TIMEOUT_MS): a rank did not join");
+        }
+    } else {
+        st->cv.wait(lk, [&] { return st->done; });
     }
+    if (st->r != ncclSuccess)
+        return nas::fail(ctx, NAS_ERR_COMM, std::string(st->what) + ": " + ncclGetErrorString(st->r));
+    ctx->comm = reinterpret_cast<ncclComm *>(st->comm);
+    ctx->comm2 = reinterpret_cast<ncclComm *>(st->comm2);
+    ctx->comm_c = reinterpret_cast<ncclComm *>(st->comm_c);
     return NAS_OK;
 }
 

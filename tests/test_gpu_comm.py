@@ -62,3 +62,19 @@ def test_options_reject_bad_values():
         e.place()
         assert e.timings()["cost_ms"] > 0
     assert np.int32(_lib.NAS_OPT_REHEARSE_WORLD) == 3
+
+
+def test_comm_init_deadline_when_a_rank_never_joins():
+    """Rank 0 of a two-rank communicator whose rank 1 never arrives: the
+    blocking ncclCommInitRank would wait forever; nas_comm_init returns
+    NAS_ERR_COMM at the deadline instead, and the context stays usable
+    without a communicator."""
+    with Engine(0) as e:
+        e.set_option("COMM_TIMEOUT_MS", 3000)
+        with pytest.raises(NasError) as ei:
+            e.comm_init(Engine.comm_unique_id(), 0, 2)
+        assert ei.value.code == _lib.NAS_ERR_COMM
+        assert "not built within 3000 ms" in str(ei.value)
+        e.synth_cluster(9, 512, 2048, "i8", peers=8)
+        node, _, _ = e.place()
+        assert (node >= -1).all()
