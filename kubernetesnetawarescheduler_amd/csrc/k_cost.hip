@@ -91,6 +91,20 @@ template <int DT>
 constexpr int cost_nwn() {
     return DT == NAS_DT_I8 ? COST_NWN_I8 : COST_NWN_BF16;
 }
+// the main scoring pass (no rescore window) on the wide tile: 256 nodes x
+// 384 pods per 12-wave workgroup (3 waves per SIMD, each 128 x 64 as in the
+// 8-wave layout, 160 KiB of LDS double buffer), 17% fewer staged bytes per
+// MAC than 256 x 256
+#ifndef COST_WIDE_I8
+#define COST_WIDE_I8 1
+#endif
+#ifndef COST_WIDE_BF16
+#define COST_WIDE_BF16 1
+#endif
+template <int DT>
+constexpr bool cost_wide() {
+    return DT == NAS_DT_I8 ? COST_WIDE_I8 : COST_WIDE_BF16;
+}
 
 template <int DT>
 struct Mma;
@@ -183,12 +197,17 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
             Ovf ov, const int *__restrict__ rowmap) {
     static_assert(!RMAP || PIPE == 0, "the row map is wired into the LDS-DMA staging only");
-    static_assert(NWN == 4 || (NWN == 2 && PIPE == 0 && (SCHED == 0 || SCHED == 2)),
-                  "the 4-wave layout has the two-stage LDS-DMA pipeline only");
-    constexpr int NW = 2 * NWN;     // waves
-    constexpr int NI = 8 / NWN;     // 32-pod MFMA tiles per wave
-    constexpr int WPODS = 32 * NI;  // pods per wave
-    constexpr int PPW = 32 / NW;    // 1 KiB LDS-DMA pieces per operand per wave per stage
+    static_assert(NWN == 4 || ((NWN == 2 || NWN == 6) && PIPE == 0 && (SCHED == 0 || SCHED == 2)),
+                  "the 4- and 12-wave layouts have the two-stage LDS-DMA pipeline only");
+    static_assert(NWN != 6 || (!RMAP && EPI == 0), "the wide tile serves the main pass only");
+    constexpr int NW = 2 * NWN;              // waves
+    constexpr int NI = NWN == 2 ? 4 : 2;     // 32-pod MFMA tiles per wave
+    constexpr int WPODS = 32 * NI;           // pods per wave
+    constexpr int BNK = NWN * WPODS;         // pods per tile (256; the wide tile 384)
+    constexpr int STG = (BM + BNK) * BKB;    // bytes per LDS stage (PIPE 0)
+    constexpr int PPWA = (BM / 8 + NW - 1) / NW;   // 1 KiB LDS-DMA pieces of A per wave per stage
+    constexpr int PPWB = (BNK / 8 + NW - 1) / NW;  // ... of B
+    constexpr int PPW = PPWB;
     using M = Mma<DT>;
     using acc_t = typename M::acc_t;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -230,14 +249,18 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         if (s < 0) return;
         if (dyn_hi_ptr) dyn_hi = dyn_hi_ptr[cb * STATUS_INTS];
         p0 = s / BN * BN;
-        if (p0 + nt * BN >= dyn_hi) return;  // whole block: before any barrier
+        if (p0 + nt * BNK >= dyn_hi) return;  // whole block: before any barrier
     }
+    // the wide tile (BNK = 384 over a launch of 256-pod units): pods at and
+    // past p_end (= dyn_hi, the launch's end) read rows past it (the next
+    // launch's, or the WA_PAD_ROWS padding) and are never written
+    const int p_end = (BNK != BN && !dyn_start) ? dyn_hi : 0x7fffffff;
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w / NWN, wn = w % NWN;
 
     const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
-    const unsigned char *Bg = WA + (size_t)(p0 + nt * BN) * Kb;
+    const unsigned char *Bg = WA + (size_t)(p0 + nt * BNK) * Kb;
     if constexpr (EPI == 3) {  // diagnostic: every block streams tile (0, 0): all L2 hits
         Ag = Lt;
         Bg = WA;
@@ -253,14 +276,15 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // buffer b of operand A / B (PIPE 0: A|B interleaved per stage; PIPE 1:
     // A0 A1 B0 B1 B2)
     auto abuf = [&](int b) -> unsigned char * {
-        return PIPE != 1 ? lds + b * STAGE_BYTES : lds + b * TILE_BYTES;
+        return PIPE != 1 ? lds + b * STG : lds + b * TILE_BYTES;
     };
     auto bbuf = [&](int b) -> unsigned char * {
-        return PIPE != 1 ? lds + b * STAGE_BYTES + TILE_BYTES : lds + (2 + b) * TILE_BYTES;
+        return PIPE != 1 ? lds + b * STG + TILE_BYTES : lds + (2 + b) * TILE_BYTES;
     };
     // one 1 KiB LDS-DMA piece (8 rows x 128 B) of operand A / B: piece j of
     // wave w fills rows (NW*j + w)*8 .. +8
     auto pieceA = [&](int buf, int k0, int j) {
+        if (BM / 8 % NW && j * NW + w >= BM / 8) return;
         const int r0 = (j * NW + w) * 8;
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
@@ -270,22 +294,45 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     if constexpr (RMAP) {
 #pragma unroll
         for (int j = 0; j < PPW; ++j)
-            bpod[j] = rowmap[min(p0 + nt * BN + (j * NW + w) * 8 + srow_in, dyn_hi - 1)];
+            bpod[j] = rowmap[min(p0 + nt * BNK + (j * NW + w) * 8 + srow_in, dyn_hi - 1)];
     }
     auto pieceB = [&](int buf, int k0, int j) {
+        if (BNK / 8 % NW && j * NW + w >= BNK / 8) return;
         const int r0 = (j * NW + w) * 8;
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
         const unsigned char *src = RMAP ? WA + (size_t)bpod[j] * Kb : Bg + (size_t)row * Kb;
         glds16<COST_AUX_B>(src + k0 + c * 16, bbuf(buf) + r0 * BKB);
     };
+    // the wide tile stages A rows then B rows as one run of 80 pieces (the
+    // B image follows the A image in LDS); piece pj of wave wu is 8 rows at
+    // pj * 8, and since pj = 12 j + wu has the parity of wu, every piece of a
+    // wave has the same swizzled lane offset: one VGPR, the row base uniform
+    // (3 waves per SIMD leave 168 registers, 128 of them accumulators)
+    const int wu = __builtin_amdgcn_readfirstlane(w);
+    const unsigned loff = (unsigned)(srow_in * Kb) +
+                          ((unsigned)(sq ^ ((4 * (wu & 1) + (srow_in >> 1)) & 7)) << 4);
+    auto piece6 = [&](int buf, int k0, int j) {
+        const int pj = j * NW + wu;
+        if (pj >= (BM + BNK) / 8) return;
+        const unsigned char *base = pj < BM / 8 ? Ag + (size_t)pj * 8 * Kb
+                                                : Bg + (size_t)(pj - BM / 8) * 8 * Kb;
+        glds16<0>(base + k0 + loff, lds + buf * STG + pj * 8 * BKB);
+    };
     auto stageA = [&](int buf, int k0) {
+        if constexpr (NWN == 6) {
 #pragma unroll
-        for (int j = 0; j < PPW; ++j) pieceA(buf, k0, j);
+            for (int j = 0; j < ((BM + BNK) / 8 + NW - 1) / NW; ++j) piece6(buf, k0, j);
+        } else {
+#pragma unroll
+            for (int j = 0; j < PPWA; ++j) pieceA(buf, k0, j);
+        }
     };
     auto stageB = [&](int buf, int k0) {
+        if constexpr (NWN != 6) {  // (the wide tile's stageA stages both)
 #pragma unroll
-        for (int j = 0; j < PPW; ++j) pieceB(buf, k0, j);
+            for (int j = 0; j < PPW; ++j) pieceB(buf, k0, j);
+        }
     };
 
     // the epilogue's fit-mask words, loaded now so their latency hides
@@ -296,7 +343,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
             for (int mi2 = 0; mi2 < 2; ++mi2) {
-                const int pod = p0 + nt * BN + wn * WPODS + ni * 32 + (lane & 31);
+                const int pod = min(p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31), p_end - 1);
                 const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
                 mwp[ni][mi2] = mask[(size_t)chunk * Pp + pod];
             }
@@ -317,9 +364,9 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
 #pragma unroll
             for (int ni = 0; ni < NI; ++ni) {
-                const int r = p0 + nt * BN + wn * WPODS + ni * 32 + (lane & 31);
+                const int r = p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31);
                 int beg = 0, end = 0;
-                if (r < cnt_lim) {
+                if (r < cnt_lim && r < p_end) {
                     const int pod = (ov.row_pod ? ov.row_pod[r] : r) + cb * Pp;
                     beg = ov.ptr[pod];
                     end = ov.ptr[pod + 1];
@@ -793,7 +840,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             for (int j = 0; j < 8; ++j) other[j] = s[j];
             merge88(mine, other);
             b = umin64(umin64(b, s[8]), mine[7]);
-            const int pod = p0 + nt * BN + wn * WPODS + rr * 64 + lane;
+            const int pod = p0 + nt * BNK + wn * WPODS + rr * 64 + lane;
+            if (pod >= p_end) return;
             store8(partial + ((size_t)mt * Pp + pod) * KC, mine);
             pbound[(size_t)mt * Pp + pod] = b;
         };
@@ -881,19 +929,23 @@ NAS_INST(0, 0, 0, 2) NAS_INST(0, 0, 0, 16)
 
 #endif
 
-template <int DT, bool RMAP>
+template <int DT, bool RMAP, int NWN = cost_nwn<DT>()>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,
                          int p0, int np, const uint64_t *mask, uint64_t *partial,
                          uint64_t *pbound, int node_base, const Dyn *dyn, int batch,
                          const Ovf &ov, const int32_t *rowmap) {
-    constexpr int NWN = cost_nwn<DT>();
+    constexpr int BNK = NWN * (NWN == 2 ? 128 : 64);
     const void *fn = reinterpret_cast<const void *>(
         &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP, NWN>);
-    const int lds = lds_bytes<COST_PIPE>();
+    const int lds = NWN == 6 ? 2 * (BM + BNK) * BKB : lds_bytes<COST_PIPE>();
     static std::atomic<unsigned long long> attr_set{0};
     hipError_t e = set_lds_once(fn, lds, attr_set);
     if (e != hipSuccess) return e;
-    const int n_mt = Mp / BM, n_nt = np / BN;
+    const int n_mt = Mp / BM, n_nt = (np + BNK - 1) / BNK;
+    // the wide tile's last pod tile reads up to WA_PAD_ROWS rows past the
+    // launch; past the last cluster's Pp rows only the padding is allocated
+    if (NWN == 6 && (int64_t)p0 + (int64_t)n_nt * BNK > (int64_t)Pp + WA_PAD_ROWS)
+        return hipErrorInvalidValue;
     auto *lt = static_cast<const unsigned char *>(Lt);
     auto *wa = static_cast<const unsigned char *>(WA);
     auto *mk = reinterpret_cast<const u64 *>(mask);
@@ -902,24 +954,34 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const int *ds = dyn ? dyn->start : nullptr;
     const int dh = dyn ? dyn->hi : 0;
     const int *dhp = dyn ? dyn->hi_ptr : nullptr;
+    // the wide tile's launch end rides in dyn_hi (unused without a window)
+    const int dhi = NWN == 6 ? p0 + np : dh;
     k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP, NWN><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
-        lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dh, dhp, ov, rowmap);
+        lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dhi, dhp, ov, rowmap);
     return hipGetLastError();
 }
 
 }  // namespace
+
+int cost_tile_pods(int dtype) {
+    const bool wide = dtype == NAS_DT_I8 ? cost_wide<NAS_DT_I8>() : cost_wide<NAS_DT_BF16>();
+    return wide ? 384 : BN;
+}
 
 // Kp: padded contraction length in ELEMENTS; np: pods, multiple of BN,
 // p0 + np <= Pp; Mp multiple of BM.
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base, const Dyn *dyn,
-                            int batch, const Ovf *ovf, const int32_t *rowmap) {
+                            int batch, const Ovf *ovf, const int32_t *rowmap, bool wide) {
     const Ovf ov = ovf ? *ovf : Ovf{};
     if (rowmap && (!dyn || batch != 1)) return hipErrorInvalidValue;
 #define NAS_COST_DISPATCH(DTV, KB, OVV)                                                            \
     (rowmap ? launch_cost_t<DTV, true>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound,     \
                                        node_base, dyn, batch, OVV, rowmap)                        \
+     : (!dyn && wide && cost_wide<DTV>())                                                                 \
+            ? launch_cost_t<DTV, false, 6>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound, \
+                                           node_base, dyn, batch, OVV, nullptr)                   \
             : launch_cost_t<DTV, false>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound,    \
                                         node_base, dyn, batch, OVV, nullptr))
     if (dyn) {  // tiles covering any window [s, s + win) clipped to hi: one extra for the offset

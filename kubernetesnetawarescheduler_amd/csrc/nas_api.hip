@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <new>
+#include <numeric>
 #include <thread>
 #include <vector>
 
@@ -308,7 +309,7 @@ int prepare_split(nas_ctx *ctx) {
     if (ctx->dtype != NAS_DT_F32 || ctx->split_valid) return NAS_OK;
     const int64_t lrows = (int64_t)ctx->B * ctx->Mp, wrows = (int64_t)ctx->B * ctx->Pp;
     OK(nas::ensure(ctx, ctx->Lt6, (size_t)lrows * 6 * ctx->Kp * 2));
-    OK(nas::ensure(ctx, ctx->WA6, (size_t)wrows * 6 * ctx->Kp * 2));
+    OK(nas::ensure(ctx, ctx->WA6, (size_t)(wrows + nas::WA_PAD_ROWS) * 6 * ctx->Kp * 2));
     HIPCK(nas::launch_split6(ctx->stream, ctx->Lt.as<float>(), ctx->Lt6.as<uint16_t>(), lrows,
                              ctx->Kp, 0));
     HIPCK(nas::launch_split6(ctx->stream, ctx->WA.as<float>(), ctx->WA6.as<uint16_t>(), wrows,
@@ -318,17 +319,33 @@ int prepare_split(nas_ctx *ctx) {
 }
 
 // one cost/top-k launch over the main traffic rows (or a row-mapped view)
+// The wide cost tile (256 nodes x 384 pods, 12 waves) for the main scoring
+// pass of one whole cluster with many pods: the full launch 3.5% (int8) / 6%
+// (bf16) faster, the C3 pass equal (int8) / 9% faster (bf16); on node shards
+// (G = 8 rehearsal: 1.61-1.66 vs 1.42-1.49 ms -- longer workgroups, coarser
+// tails) and on batches of small clusters (C5: 5,000 pods = 13.02 wide tiles)
+// it loses, so those keep the 256 x 256 tile (profiles/r02_s4_ab_wide*.txt)
+constexpr int WIDE_MIN_PODS = 32768;
+bool wide_ok(const nas_ctx *ctx) {
+    return ctx->B == 1 && ctx->world == 1 && ctx->rehearse == 0 && ctx->Pp >= WIDE_MIN_PODS;
+}
+int tile_pods(const nas_ctx *ctx) {
+    return wide_ok(ctx) ? nas::cost_tile_pods(ctx->dtype == NAS_DT_F32 ? NAS_DT_BF16 : ctx->dtype)
+                        : nas::COST_BN;
+}
+
 hipError_t launch_cost(nas_ctx *ctx, hipStream_t st, int Pp, int p0, int np, const uint64_t *mask,
                        const nas::Dyn *dyn, int batch, const nas::Ovf *ov,
                        const int32_t *rowmap = nullptr) {
+    const bool wide = wide_ok(ctx);
     if (ctx->dtype == NAS_DT_F32)
         return nas::launch_cost_topk(st, NAS_DT_BF16, ctx->Lt6.p, ctx->WA6.p, ctx->Mp, 6 * ctx->Kp,
                                      Pp, p0, np, mask, ctx->partial.as<uint64_t>(),
                                      ctx->pbound.as<uint64_t>(), ctx->Nloc0, dyn, batch, nullptr,
-                                     rowmap);
+                                     rowmap, wide);
     return nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, Pp, p0, np,
                                  mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                 ctx->Nloc0, dyn, batch, ov, rowmap);
+                                 ctx->Nloc0, dyn, batch, ov, rowmap, wide);
 }
 
 // exact traffic row (n values, each within int32) -> the int8 plane row and
@@ -775,6 +792,11 @@ void inject_stall(nas_ctx *ctx, hipStream_t st) {
 // about 32, so the commit left after the scoring ends (the serial tail, which
 // matters most on a node shard's short scoring) is short.
 constexpr int CHUNK_WORKGROUPS = 512;  // cost workgroups per big chunk (measured best)
+#ifndef CHUNK_TILES_WIDE
+#define CHUNK_TILES_WIDE 48  // 256-pod units per chunk on the wide tile: 32 tiles of 384 (1,280
+                             // workgroups at 40 node tiles, as the 256-pod form's 32-unit chunks);
+                             // 24 / 33 units measured 0.5-2% slower (profiles/r02_s4_ab_chunk.txt)
+#endif
 int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     const int wgs = CHUNK_WORKGROUPS;
     const int n_mt = ctx->Mp / nas::COST_BM;
@@ -787,6 +809,7 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     const int mode = big > 32 ? 2 : 0;
     const int left = (ctx->P - lo + nas::COST_BN - 1) / nas::COST_BN;  // pod tiles left
     int tiles = c == 0 ? 32 : big;
+    if (tile_pods(ctx) != nas::COST_BN) tiles = CHUNK_TILES_WIDE;  // (one cluster, G = 1)
     // a pass whose pods fit one big chunk (C2: 40 pod tiles on 4 node tiles)
     // is one chunk: pipelining its short tail would save less than the
     // cross-stream hops and launches it adds (device time 0.96 -> 0.92 ms, C2)
@@ -803,6 +826,10 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
         const int n = (left + big - 1) / big;
         tiles = (left + n - 1) / n;
     }  // (decreasing chunk sizes n, n-1, ..., 1 measured 7-10% slower at G = 4 / 8)
+    // whole cost tiles per chunk: the wide tile (384 pods) needs multiples of
+    // 3 units, or a chunk's last tile would score pods of the next chunk
+    const int unit = tile_pods(ctx) / std::gcd(tile_pods(ctx), nas::COST_BN);
+    tiles = std::min(left, (tiles + unit - 1) / unit * unit);
     return tiles * nas::COST_BN;
 }
 
@@ -1351,7 +1378,7 @@ static int traffic_common(nas_ctx *ctx, int32_t dtype, int32_t P, int32_t n) {
     ctx->P = P;
     ctx->Pp = (int32_t)nas::round_up(P, nas::COST_BN);
     const size_t wa_bytes = (size_t)ctx->B * ctx->Pp * ctx->Kp * esz(dtype);
-    OK(nas::ensure(ctx, ctx->WA, wa_bytes));
+    OK(nas::ensure(ctx, ctx->WA, wa_bytes + (size_t)nas::WA_PAD_ROWS * ctx->Kp * esz(dtype)));
     HIPCK(hipMemsetAsync(ctx->WA.p, 0, wa_bytes, ctx->stream));
     ctx->wa_P = P;
     ctx->wa_n = n;
@@ -2192,7 +2219,7 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
     const size_t e = esz(dtype);
     const size_t lt_b = (size_t)ctx->Mp * ctx->Kp * e, wa_b = (size_t)ctx->Pp * ctx->Kp * e;
     OK(nas::ensure(ctx, ctx->Lt, lt_b * B));
-    OK(nas::ensure(ctx, ctx->WA, wa_b * B));
+    OK(nas::ensure(ctx, ctx->WA, wa_b * B + (size_t)nas::WA_PAD_ROWS * ctx->Kp * e));
     OK(nas::ensure(ctx, ctx->cap0, (size_t)B * 3 * n_nodes * 4));
     OK(nas::ensure(ctx, ctx->cap, (size_t)B * 3 * n_nodes * 4));
     OK(nas::ensure(ctx, ctx->req, (size_t)B * 3 * ctx->Pp * 4));

@@ -21,6 +21,10 @@ constexpr int KC = NAS_K_CANDIDATES;  // candidates per pod
 // Cost contraction tile (see k_cost.hip): BM nodes x BN pods, 128-byte K stage.
 constexpr int COST_BM = 256;
 constexpr int COST_BN = 256;
+// rows allocated past the last traffic row: the wide cost tile (384 pods over
+// launches of 256 k pods, ceil(256 k / 384) tiles) reads up to 256 rows past a
+// launch's end (k = 2 mod 3), whose results it discards
+constexpr int WA_PAD_ROWS = 256;
 constexpr int COST_BKB = 128;  // bytes of K per stage (128 int8 or 64 bf16)
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
@@ -221,11 +225,14 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
                       const Dyn *dyn = nullptr, int batch = 1, const int32_t *rowmap = nullptr,
                       int req_stride = 0);
 
+// pods per tile of the wide cost kernel for this (compute) dtype when it is
+// built in (384), else COST_BN
+int cost_tile_pods(int dtype);
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base,
                             const Dyn *dyn = nullptr, int batch = 1, const Ovf *ovf = nullptr,
-                            const int32_t *rowmap = nullptr);
+                            const int32_t *rowmap = nullptr, bool wide = false);
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,
