@@ -59,6 +59,12 @@ constexpr int TILE_BYTES = BM * BKB;          // 32 KiB: one operand, one stage
 #ifndef COST_GM
 #define COST_GM (-4)
 #endif
+// the wide tile's order: pod groups of 2 (2 x 384 pods x every node tile):
+// C3 pass 8.04-8.09 vs 8.09-8.12 ms for groups of 4 (launch equal), groups
+// of 1 / 3 / 8 and node-group-major 2 / 8 slower (profiles/r02_s4_ab_gm.txt)
+#ifndef COST_GM_WIDE
+#define COST_GM_WIDE (-2)
+#endif
 // PIPE 0: A and B double-buffered (128 KiB).  PIPE 1: A (latency rows, mostly
 // L2/MALL-resident) double-buffered, B (the 1 GB traffic stream, mostly HBM)
 // triple-buffered so its loads get two K-steps of cover (160 KiB, all of LDS).
@@ -936,7 +942,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
                          const Ovf &ov, const int32_t *rowmap) {
     constexpr int BNK = NWN * (NWN == 2 ? 128 : 64);
     const void *fn = reinterpret_cast<const void *>(
-        &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP, NWN>);
+        &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, NWN == 6 ? COST_GM_WIDE : COST_GM, RMAP, NWN>);
     const int lds = NWN == 6 ? 2 * (BM + BNK) * BKB : lds_bytes<COST_PIPE>();
     static std::atomic<unsigned long long> attr_set{0};
     hipError_t e = set_lds_once(fn, lds, attr_set);
@@ -956,7 +962,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const int *dhp = dyn ? dyn->hi_ptr : nullptr;
     // the wide tile's launch end rides in dyn_hi (unused without a window)
     const int dhi = NWN == 6 ? p0 + np : dh;
-    k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, COST_GM, RMAP, NWN><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
+    k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, NWN == 6 ? COST_GM_WIDE : COST_GM, RMAP, NWN><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
         lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dhi, dhp, ov, rowmap);
     return hipGetLastError();
 }
