@@ -61,7 +61,7 @@ def parse():
                          "(its node columns; the other ranks' lists are shifted copies of its "
                          "own; placements not meaningful, RCCL over a one-rank communicator)")
     ap.add_argument("--only", choices=["place", "vote", "score", "pmc", "C1", "C2", "C2_f32",
-                                       "C3_bf16", "C5", "C4"], default=None,
+                                       "C3_bf16", "C5", "C4", "C4_shardG2"], default=None,
                     help="profile helper: run only one path (pmc: the score and vote legs, "
                          "what the in-run PMC passes profile)")
     ap.add_argument("--no-pmc", action="store_true",
@@ -334,6 +334,31 @@ def bench_cost_kernel(args, d, eng):
         assert t["cost_launches"] == 1
         ms.append(t["cost_ms"])
     return float(np.mean(ms)), ms
+
+
+def bench_fit_kernel(args, d, eng, reps=10):
+    """Roofline of the resource-fit filter (north star kernel (1)): the
+    standalone nas_filter over all pod x node pairs of the workload (one k_fit
+    launch, HIP events around it on its stream).  In the placement pass the
+    wide cost tile decides the fit itself (k_cost.hip, fused fit); this is the
+    filter as its own HBM-bound kernel.  Algorithmic bytes: the mask written
+    once (P x ceil(N/64) x 8 B) plus capacities and requests read once."""
+    N, P = args.nodes, args.pods
+    nloc = (d.rank + 1) * N // d.world - d.rank * N // d.world
+    eng.reset_capacity()
+    eng.filter(want_mask=False)  # warm-up
+    ms = []
+    for _ in range(reps):
+        eng.filter(want_mask=False)
+        ms.append(eng.timings()["fit_ms"])
+    fit_ms = float(np.mean(ms))
+    algo = P * ((nloc + 63) // 64) * 8.0 + 3 * 4.0 * (nloc + P)
+    return {"kernel": "k_fit (nas_filter, standalone)", "bound": "hbm",
+            "achieved": algo / (fit_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": algo / (fit_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "launch_ms": fit_ms,
+            "launch_ms_min": min(ms), "launches": reps, "bytes_per_launch": algo,
+            "note": "mask write P*ceil(N/64)*8 B + capacities and requests 12*(N+P) B per launch; "
+                    "HIP events around the one launch"}
 
 
 def vendor_gemm_reference(args, d, reps=5):
@@ -831,6 +856,8 @@ def config_c4(args, d, eng, N=50000, P=500000):
     eng.synth_cluster(SEED, N, P, "i8", peers=args.peers)
     steps = max(1, min(args.steps, 2))
     t, res = _timed_place(d, eng, steps, 1)
+    if d.world == 1:
+        _C4_WORLD1.update(node=res["node"].copy(), score=res["score"].copy())
     ms = t * 1e3 / steps
     # pass-level roofline: 2 * P * N * K int8 ops per pass (K = N padded to
     # 128) over the whole pass's wall time -- the cost launches (two scoring
@@ -856,12 +883,59 @@ def config_c4(args, d, eng, N=50000, P=500000):
     return out
 
 
+_C4_WORLD1 = {}
+
+
+def config_c4_shard(args, d, eng, G=2, N=50000, P=500000):
+    """configs[3]'s node split at its own size on ONE GPU: G virtual node
+    shards (nas_set_shard contexts, each scoring N/G node columns over the full
+    K), lists exchanged and merged on the host, the commit replayed on every
+    shard (sharded.place_local_shards).  The shards run one after another on
+    the same GPU, so this is G x one shard's work plus the host exchange -- a
+    check of the multi-GPU split's geometry and results at size, NOT a
+    multi-GPU timing.  Placements and scores are compared with the world-1
+    C4 pass of the same seed (configs.C4, same run)."""
+    from kubernetesnetawarescheduler_amd import Engine
+    from kubernetesnetawarescheduler_amd.sharded import place_local_shards
+    engines = [eng] + [Engine(d.local) for _ in range(G - 1)]
+    try:
+        for r, e in enumerate(engines):
+            e.set_shard(r, G)
+            e.synth_cluster(SEED, N, P, "i8", peers=args.peers)
+        res = {}
+
+        def step():
+            for e in engines:
+                e.reset_capacity()
+            res["node"], res["score"], res["rounds"] = place_local_shards(engines, P)
+
+        t = time_steps(d, step, 1, 1)
+        caps = [e.get_capacity() for e in engines]
+    finally:
+        for e in engines[1:]:
+            e.close()
+    ms = t * 1e3
+    out = {"workload": f"C4: {N} nodes x {P} pods as {G} virtual node shards on one GPU, "
+                       f"host exchange (sharded.place_local_shards)",
+           "value": P * N / (ms * 1e-3), "unit": "pair-scores/s", "ms_per_step": ms, "steps": 1,
+           "rescore_rounds": res["rounds"], "unschedulable": int((res["node"] < 0).sum()),
+           "shards_agree_on_capacity": bool(all((c == caps[0]).all() for c in caps)),
+           "note": "the G shards' scoring runs serially on one GPU and the lists cross the host: "
+                   "a correctness run of the multi-GPU split at its size, not a scaling number"}
+    w1 = _C4_WORLD1.get("node")
+    if w1 is not None:
+        out["equals_world1"] = bool((w1 == res["node"]).all() and
+                                    (_C4_WORLD1["score"] == res["score"]).all())
+    return out
+
+
 def run_configs(args, d, only=None):
     """The other BASELINE configs, each on a fresh context (one GPU)."""
     from kubernetesnetawarescheduler_amd import Engine
     out = {}
     for name, fn in (("C1", config_c1), ("C2", config_c2), ("C2_f32", config_c2_f32),
-                     ("C3_bf16", config_c3_bf16), ("C5", config_c5), ("C4", config_c4)):
+                     ("C3_bf16", config_c3_bf16), ("C5", config_c5), ("C4", config_c4),
+                     ("C4_shardG2", config_c4_shard)):
         if only and name != only:
             continue
         with Engine(d.local) as e:
@@ -953,10 +1027,11 @@ def main():
                                    "it with the rocprofv3 kernel trace of the same command"}
         if d.gpu and d.world == 1 and args.only is None:
             out["roofline"]["vendor_gemm"] = vendor_gemm_reference(args, d)
-    if traffic.get("k_fit"):
-        fb = 2.0 * N * 4 * 3 + 2.0 * P * 4 * 3 + P * ((N + 63) // 64) * 8.0  # capacities, requests, mask
-        out["fit_traffic"] = {"kernel": "k_fit", "bytes": traffic["k_fit"]["bytes"],
-                              "algorithmic_bytes": fb, "unit": "B/launch"}
+    if args.only not in ("vote",) and d.gpu:
+        fr = bench_fit_kernel(args, d, eng)
+        fr["traffic"] = traffic.get("k_fit", {}).get("bytes")
+        fr["traffic_unit"] = "B/launch"
+        out["fit_roofline"] = fr
     if not args.no_reference_mode and args.only in (None, "vote", "pmc"):
         elapsed, vote_ms, S, ref = bench_vote(args, d, eng)
         pods_total = S if args.vote_node_shard else S * d.world

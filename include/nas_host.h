@@ -54,7 +54,9 @@ int nas_host_node_metrics(const char *body, size_t n, const char *node, double *
  * bytes) under name names[i], each as nas_host_node_metrics, into SoA
  * arrays ready for nas_upload_snapshot (bandwidth comes from the iperf
  * reports, so the caller fills it).  status[i] = NAS_OK or NAS_HOST_PANIC
- * (that node's values are then 0: the reference would have crashed).  The
+ * (that node's values are then 0: the reference would have crashed), or
+ * NAS_ERR_STATE for a failure that is not a reference behaviour (e.g. out of
+ * memory; values 0, and the call then returns NAS_ERR_STATE).  The
  * nodes are split over `threads` worker threads (<= 0: the hardware's
  * concurrency); the results do not depend on the thread count.  Replaces the
  * reference's per-pod sequential scrape-and-parse of :275-331 with one

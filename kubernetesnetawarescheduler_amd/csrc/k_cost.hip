@@ -195,17 +195,18 @@ struct Top4 {
 // (read in place by the LDS-DMA source addresses; rows past the view's count
 // read its last row and are never merged)
 template <int DT, int EPI = 0, int SCHED = COST_SCHED, int PIPE = COST_PIPE, int GM = COST_GM,
-          bool RMAP = false, int NWN = 4>
+          bool RMAP = false, int NWN = 4, bool FUSE = (NWN == 6)>
 __global__ void __launch_bounds__(128 * NWN, 1)
 k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
             u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base,
             const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
-            Ovf ov, const int *__restrict__ rowmap) {
+            Ovf ov, const int *__restrict__ rowmap, FitSrc fs) {
     static_assert(!RMAP || PIPE == 0, "the row map is wired into the LDS-DMA staging only");
     static_assert(NWN == 4 || ((NWN == 2 || NWN == 6) && PIPE == 0 && (SCHED == 0 || SCHED == 2)),
                   "the 4- and 12-wave layouts have the two-stage LDS-DMA pipeline only");
-    static_assert(NWN != 6 || (!RMAP && EPI == 0), "the wide tile serves the main pass only");
+    static_assert(NWN != 6 || (!RMAP && EPI == 0 && FUSE), "the wide tile serves the main pass only");
+    static_assert(!FUSE || (!RMAP && EPI == 0 && PIPE == 0), "the fused fit: main-range launches");
     constexpr int NW = 2 * NWN;              // waves
     constexpr int NI = NWN == 2 ? 4 : 2;     // 32-pod MFMA tiles per wave
     constexpr int WPODS = 32 * NI;           // pods per wave
@@ -245,6 +246,10 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         nt = first_nt + r % pg;
     }
     const int cb = blockIdx.y;  // cluster of a batched launch
+    if constexpr (FUSE) {
+        fs.cap += (size_t)cb * 3 * fs.N;
+        fs.req += (size_t)cb * 3 * Pp;
+    }
     Lt += (size_t)cb * n_mt * BM * Kb;  // (tile order above: speed only)
     WA += (size_t)cb * Pp * Kb;
     mask += (size_t)cb * (n_mt * BM / 64) * Pp;
@@ -341,10 +346,82 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         }
     };
 
+    // Fused fit (main-range launches: the pass's chunks launch back to back
+    // with no k_fit between them -- a fit launch in front of every cost
+    // launch could not start until a wide workgroup drained its CU, and the
+    // cost launch behind it then waited too).  The workgroup decides the fit
+    // words itself, exactly as k_fit does, after its main loop: per 64-node
+    // chunk the minima / maxima of the free capacity (read then -- after the
+    // previous chunks' commits and possibly during this chunk's predecessor's;
+    // capacity only shrinks, so a "does not fit" read at any earlier time
+    // still holds at the pod's turn) decide every pod that fits all valid
+    // nodes or none; the rest compare against the lanes' capacities (three
+    // ballots).  The words land where the k_fit mask words would (mwp).
+    int rq[FUSE ? NI : 1][3];
+    int fcap[2][3];
+    auto fit_issue = [&]() {  // the requests of the lane's pods, its nodes' capacities
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+            const int pod = min(p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31), p_end - 1);
+#pragma unroll
+            for (int r = 0; r < 3; ++r) rq[ni][r] = fs.req[(size_t)r * Pp + pod];
+        }
+#pragma unroll
+        for (int mi2 = 0; mi2 < 2; ++mi2) {
+            const int nl = mt * BM + wm * 128 + mi2 * 64 + lane;
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+                fcap[mi2][r] = nl < fs.nloc ? __hip_atomic_load(const_cast<int *>(fs.cap) + (size_t)r * fs.N + fs.n0 + nl,
+                                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : -1;
+        }
+    };
+    // fit words: bit j of mw[ni][mi2] = the lane's pod of group ni fits node
+    // wm*128 + mi2*64 + j of the tile
+    auto fit_words = [&](u64 (&mw)[NI][2]) {
+#pragma unroll
+        for (int mi2 = 0; mi2 < 2; ++mi2) {
+            const bool real = mt * BM + wm * 128 + mi2 * 64 + lane < fs.nloc;
+            const u64 valid = __builtin_amdgcn_ballot_w64(real);
+            int mn[3], mx[3];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                int a = real ? fcap[mi2][r] : 0x7fffffff, x = real ? fcap[mi2][r] : (int)0x80000000;
+#pragma unroll
+                for (int o = 32; o; o >>= 1) {
+                    a = min(a, __shfl_xor(a, o));
+                    x = max(x, __shfl_xor(x, o));
+                }
+                mn[r] = __builtin_amdgcn_readfirstlane(a);
+                mx[r] = __builtin_amdgcn_readfirstlane(x);
+            }
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) {
+                const int a = rq[ni][0], bq = rq[ni][1], d = rq[ni][2];
+                const bool all = a <= mn[0] && bq <= mn[1] && d <= mn[2];
+                const bool none = a > mx[0] || bq > mx[1] || d > mx[2];
+                u64 word = all ? valid : 0ull;
+                // lanes l and l + 32 hold the same pod: decide lanes 0..31
+                u64 rest = __builtin_amdgcn_ballot_w64(!all && !none) & 0xffffffffull;
+                while (rest) {
+                    const int i = (int)__builtin_ctzll(rest);
+                    rest &= rest - 1;
+                    const int ra = __builtin_amdgcn_readlane(a, i), rb = __builtin_amdgcn_readlane(bq, i);
+                    const int rd = __builtin_amdgcn_readlane(d, i);
+                    const u64 m = __builtin_amdgcn_ballot_w64(ra <= fcap[mi2][0]) &
+                                  __builtin_amdgcn_ballot_w64(rb <= fcap[mi2][1]) &
+                                  __builtin_amdgcn_ballot_w64(rd <= fcap[mi2][2]);
+                    if ((lane & 31) == i) word = m;
+                }
+                mw[ni][mi2] = word;
+            }
+        }
+    };
+
     // the epilogue's fit-mask words, loaded now so their latency hides
     // under the main loop (k_fit wrote them before this launch)
     u64 mwp[NI][2];
-    if constexpr (EPI == 0 || EPI == 2 || EPI == 6) {
+    if constexpr (!FUSE && (EPI == 0 || EPI == 2 || EPI == 6)) {
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
@@ -712,6 +789,14 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             }
         return;
     }
+    if constexpr (FUSE) {
+        // the fused fit, after the main loop: nothing of it is live across
+        // the loop (held there, its registers pushed the loop's LDS-DMA
+        // addresses into scratch: the launch ran 12-24% slower); the loads'
+        // latency (~1 us of L2) is exposed once per workgroup
+        fit_issue();
+        fit_words(mwp);
+    }
     // ---- epilogue: fit mask + per-pod candidate list
     // per lane: top-4 of its 64 (node, cost) values per pod; lanes l and l^32
     // (same pod, complementary rows) merge into a sorted 8-list whose bound is
@@ -923,7 +1008,7 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
 #define NAS_INST(E, S, PP, G)                                                                      \
     template __global__ void k_cost_topk<NAS_DT_I8, E, S, PP, G>(                                  \
         const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
-        u64 *, int, const int *, int, const int *, Ovf, const int *);
+        u64 *, int, const int *, int, const int *, Ovf, const int *, FitSrc);
 NAS_INST(0, 0, 0, 4) NAS_INST(1, 0, 0, 4) NAS_INST(0, 5, 0, 4) NAS_INST(1, 5, 0, 4)
 NAS_INST(3, 5, 0, 4) NAS_INST(0, 1, 0, 4) NAS_INST(0, 5, 0, 8) NAS_INST(4, 0, 0, 4)
 NAS_INST(0, 1, 2, 4) NAS_INST(0, 1, 3, 4) NAS_INST(0, 0, 2, 4) NAS_INST(0, 0, 3, 4)
@@ -935,14 +1020,14 @@ NAS_INST(0, 0, 0, 2) NAS_INST(0, 0, 0, 16)
 
 #endif
 
-template <int DT, bool RMAP, int NWN = cost_nwn<DT>()>
+template <int DT, bool RMAP, int NWN = cost_nwn<DT>(), bool FUSE = (NWN == 6)>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,
                          int p0, int np, const uint64_t *mask, uint64_t *partial,
                          uint64_t *pbound, int node_base, const Dyn *dyn, int batch,
-                         const Ovf &ov, const int32_t *rowmap) {
+                         const Ovf &ov, const int32_t *rowmap, const FitSrc &fs = FitSrc{}) {
     constexpr int BNK = NWN * (NWN == 2 ? 128 : 64);
     const void *fn = reinterpret_cast<const void *>(
-        &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, NWN == 6 ? COST_GM_WIDE : COST_GM, RMAP, NWN>);
+        &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, NWN == 6 ? COST_GM_WIDE : COST_GM, RMAP, NWN, FUSE>);
     const int lds = NWN == 6 ? 2 * (BM + BNK) * BKB : lds_bytes<COST_PIPE>();
     static std::atomic<unsigned long long> attr_set{0};
     hipError_t e = set_lds_once(fn, lds, attr_set);
@@ -951,6 +1036,9 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     // the wide tile's last pod tile reads up to WA_PAD_ROWS rows past the
     // launch; past the last cluster's Pp rows only the padding is allocated
     if (NWN == 6 && (int64_t)p0 + (int64_t)n_nt * BNK > (int64_t)Pp + WA_PAD_ROWS)
+        return hipErrorInvalidValue;
+    // the fused fit (the wide tile always): capacity and requests
+    if (FUSE && (!fs.cap || !fs.req || fs.nloc > Mp || fs.n0 + fs.nloc > fs.N || dyn))
         return hipErrorInvalidValue;
     auto *lt = static_cast<const unsigned char *>(Lt);
     auto *wa = static_cast<const unsigned char *>(WA);
@@ -962,8 +1050,8 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const int *dhp = dyn ? dyn->hi_ptr : nullptr;
     // the wide tile's launch end rides in dyn_hi (unused without a window)
     const int dhi = NWN == 6 ? p0 + np : dh;
-    k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, NWN == 6 ? COST_GM_WIDE : COST_GM, RMAP, NWN><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
-        lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dhi, dhp, ov, rowmap);
+    k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, NWN == 6 ? COST_GM_WIDE : COST_GM, RMAP, NWN, FUSE><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
+        lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dhi, dhp, ov, rowmap, fs);
     return hipGetLastError();
 }
 
@@ -979,7 +1067,10 @@ int cost_tile_pods(int dtype) {
 hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const void *WA, int Mp,
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base, const Dyn *dyn,
-                            int batch, const Ovf *ovf, const int32_t *rowmap, bool wide) {
+                            int batch, const Ovf *ovf, const int32_t *rowmap, bool wide,
+                            const FitSrc *fit) {
+    if (fit && (dyn || rowmap)) return hipErrorInvalidValue;  // windows keep the k_fit mask
+    if (!fit && wide && !dyn && !rowmap) return hipErrorInvalidValue;  // the wide tile fuses
     const Ovf ov = ovf ? *ovf : Ovf{};
     if (rowmap && (!dyn || batch != 1)) return hipErrorInvalidValue;
 #define NAS_COST_DISPATCH(DTV, KB, OVV)                                                            \
@@ -987,7 +1078,10 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
                                        node_base, dyn, batch, OVV, rowmap)                        \
      : (!dyn && wide && cost_wide<DTV>())                                                                 \
             ? launch_cost_t<DTV, false, 6>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound, \
-                                           node_base, dyn, batch, OVV, nullptr)                   \
+                                           node_base, dyn, batch, OVV, nullptr, *fit)             \
+     : fit ? launch_cost_t<DTV, false, cost_nwn<DTV>(), true>(st, Lt, WA, Mp, KB, Pp, p0, np,     \
+                                                             mask, partial, pbound, node_base,    \
+                                                             dyn, batch, OVV, nullptr, *fit)      \
             : launch_cost_t<DTV, false>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound,    \
                                         node_base, dyn, batch, OVV, nullptr))
     if (dyn) {  // tiles covering any window [s, s + win) clipped to hi: one extra for the offset

@@ -94,7 +94,13 @@ int gather_batch(int check) { return check == 2 ? 1 : GATHER_SLOTS_PER_SYNC; }
 // rescore, 0.39 -> 0.26 ms, but cost bench C1's 3-slot case two extra round
 // trips, 0.39 -> 0.52 ms: with a round trip ~2 idle slots, 4 then 1 is the
 // robust order)
-constexpr size_t HOST_OUT_OFFSET = 4096;  // pinned staging of nas_place results in host_status
+// pinned staging of nas_place results in host_status: behind the status words
+// of every cluster of a batch (B * STATUS_INTS ints; nas_set_batch allows up to
+// 65535 clusters), page-aligned
+size_t host_out_offset(int B) {
+    const size_t status_bytes = (size_t)std::max(B, 1) * (nas::STATUS_INTS + 4) * 4;
+    return std::max<size_t>(4096, (status_bytes + 4095) & ~(size_t)4095);
+}
 // Rescore slots run only for a walk known to have halted (after the
 // pipeline): an idle gathered slot still costs ~0.1 ms of launches (C3,
 // measured), more than the host round trip a stop costs once the pipeline is
@@ -334,18 +340,21 @@ int tile_pods(const nas_ctx *ctx) {
                         : nas::COST_BN;
 }
 
+// A launch over a main pod range (no rescore window, no row map) decides the
+// fit itself from `fit` (k_cost.hip: fused fit), so no k_fit launch sits
+// between two cost launches of a scoring stream; windows keep the k_fit mask.
 hipError_t launch_cost(nas_ctx *ctx, hipStream_t st, int Pp, int p0, int np, const uint64_t *mask,
                        const nas::Dyn *dyn, int batch, const nas::Ovf *ov,
-                       const int32_t *rowmap = nullptr) {
+                       const int32_t *rowmap = nullptr, const nas::FitSrc *fit = nullptr) {
     const bool wide = wide_ok(ctx);
     if (ctx->dtype == NAS_DT_F32)
         return nas::launch_cost_topk(st, NAS_DT_BF16, ctx->Lt6.p, ctx->WA6.p, ctx->Mp, 6 * ctx->Kp,
                                      Pp, p0, np, mask, ctx->partial.as<uint64_t>(),
                                      ctx->pbound.as<uint64_t>(), ctx->Nloc0, dyn, batch, nullptr,
-                                     rowmap, wide);
+                                     rowmap, wide, fit);
     return nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, Pp, p0, np,
                                  mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                 ctx->Nloc0, dyn, batch, ov, rowmap, wide);
+                                 ctx->Nloc0, dyn, batch, ov, rowmap, wide, fit);
 }
 
 // exact traffic row (n values, each within int32) -> the int8 plane row and
@@ -375,6 +384,8 @@ int check_extended(nas_ctx *ctx) {
         return nas::fail(ctx, NAS_ERR_ARG, "dtypes of latency / traffic differ");
     if (ctx->N != ctx->L_n || ctx->P != ctx->req_P || ctx->dtype != ctx->L_dtype)
         return nas::fail(ctx, NAS_ERR_STATE, "re-upload latency and traffic after resizing");
+    if (ctx->world > 1 && !ctx->comm && !ctx->virtual_shard)
+        return nas::fail(ctx, NAS_ERR_STATE, "node shard without a communicator");
     // int8 path: exact int32 costs need sum_m |WA[p,m]| * |L[m,n]| <= INT32_MAX
     if (ctx->dtype == NAS_DT_I8 && ctx->wa_abs_row_max * (int64_t)ctx->L_abs_max > 0x7fffffffLL)
         return nas::fail(ctx, NAS_ERR_UNSUPPORTED,
@@ -471,12 +482,12 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
     const int np = pr1 - pr0;
     auto *mask = ctx->mask.as<uint64_t>();
+    // the cost launch decides the fit itself (fused fit): no k_fit before it
+    const nas::FitSrc fit{cap, v.req, ctx->N, ctx->Nloc0, ctx->Nloc};
     hipEvent_t e0 = tm.fine(st);
-    HIPCK(nas::launch_fit(st, cap, ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp, v.req, p_hi, v.Pp, p_lo,
-                          p_hi - p_lo, mask));
-    hipEvent_t e1 = tm.fine(st);
+    hipEvent_t e1 = e0;
     const nas::Ovf ov = make_ovf(ctx);
-    HIPCK(launch_cost(ctx, st, v.Pp, pr0, np, mask, nullptr, 1, &ov));
+    HIPCK(launch_cost(ctx, st, v.Pp, pr0, np, mask, nullptr, 1, &ov, nullptr, &fit));
     hipEvent_t e2 = tm.fine(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
@@ -599,18 +610,18 @@ int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi, int32_t *pub = nullptr) {
     return NAS_OK;
 }
 
-// Scoring pass over every cluster of a batch: one fit, cost/top-k and merge
-// launch each, against the working capacity (cluster = a grid dimension).
+// Scoring pass over every cluster of a batch: one cost/top-k launch (with
+// the fused fit) and one merge launch, against the working capacity (cluster
+// = a grid dimension).
 int score_batch(nas_ctx *ctx, Timer &tm) {
     hipStream_t st = ctx->stream;
     const int B = ctx->B, P = ctx->P, Pp = ctx->Pp, N = ctx->N;
     auto *mask = ctx->mask.as<uint64_t>();
     hipEvent_t e0 = tm.mark(st);
-    HIPCK(nas::launch_fit(st, ctx->cap.as<int32_t>(), N, 0, N, ctx->Mp, ctx->req.as<int32_t>(), P,
-                          Pp, 0, P, mask, nullptr, B));
-    hipEvent_t e1 = tm.mark(st);
+    hipEvent_t e1 = e0;
     const nas::Ovf ov = make_ovf(ctx);
-    HIPCK(launch_cost(ctx, st, Pp, 0, Pp, mask, nullptr, B, &ov));
+    const nas::FitSrc fit{ctx->cap.as<int32_t>(), ctx->req.as<int32_t>(), N, 0, N};
+    HIPCK(launch_cost(ctx, st, Pp, 0, Pp, mask, nullptr, B, &ov, nullptr, &fit));
     hipEvent_t e2 = tm.mark(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
@@ -649,7 +660,7 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
     // every cluster's placements (and raw scores) go to the pinned stage right
     // behind the commit, before the status words: when no cluster stopped,
     // the one status round trip brings the results with it
-    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
+    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + host_out_offset(ctx->B));
     const size_t BP = (size_t)B * P;
     const bool want_raw = cost_out || int_score_out;
     auto fetch = [&]() -> int {
@@ -723,7 +734,7 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
 // Abort every communicator of a context whose collective missed its deadline:
 // the stuck collective kernels return, later calls fail fast (bind).
 void abort_comms(nas_ctx *ctx) {
-    for (ncclComm **c : {&ctx->comm, &ctx->comm2, &ctx->comm_c}) {
+    for (ncclComm **c : {&ctx->comm, &ctx->comm2, &ctx->comm_c, &ctx->comm_root}) {
         if (*c) (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(*c));
         *c = nullptr;
     }
@@ -854,10 +865,10 @@ int alloc_extended(nas_ctx *ctx) {
         OK(nas::ensure(ctx, ctx->gather_r, (size_t)ctx->world * RESCORE_PODS * KC * 8));
         OK(nas::ensure(ctx, ctx->gbound_r, (size_t)ctx->world * RESCORE_PODS * 8));
     }
-    // pinned: the status words, then (from HOST_OUT_OFFSET) a staging area for
-    // the placements and scores so their copies back are DMA, not staged
-    const size_t hs_bytes = HOST_OUT_OFFSET + 2 * B * (size_t)ctx->Pp * 4;
-    static_assert(HOST_OUT_OFFSET >= 256, "status words fit below the staging area");
+    // pinned: the status words, then (from host_out_offset(B)) a staging area
+    // for the placements and scores so their copies back are DMA, not staged,
+    // and a second one for nas_place's speculative full copy (below)
+    const size_t hs_bytes = host_out_offset((int)B) + 4 * B * (size_t)ctx->Pp * 4;
     if (ctx->host_status.bytes < hs_bytes) {
         if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
         ctx->host_status.p = nullptr;
@@ -881,6 +892,10 @@ void destroy_comms(nas_ctx *ctx) {
         if (*c) (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(*c));
         *c = nullptr;
     }
+    // the non-blocking root issued no collectives and owns nothing the
+    // children use (no splitShare): aborting it needs no peer
+    if (ctx->comm_root) (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(ctx->comm_root));
+    ctx->comm_root = nullptr;
 }
 
 }  // namespace
@@ -1683,9 +1698,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         return NAS_OK;
     };
     int32_t *hs = ctx->host_status.as<int32_t>();
-    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + HOST_OUT_OFFSET);
+    int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + host_out_offset(ctx->B));
+    // the speculative slots' full copy lands in its own area: the host may
+    // still be unpacking chunks from `stage` while that copy runs
+    int32_t *stage_spec = stage + 2 * (size_t)ctx->Pp;
     const bool want_raw = cost_out || int_score_out;
-    const uint32_t *raw = reinterpret_cast<const uint32_t *>(stage + P);  // decoded in place
     struct Landed { int lo, hi; hipEvent_t ev; };
     std::vector<Landed> landed;
     // chunk bounds; every scoring launch is enqueued before any commit-stream
@@ -1776,10 +1793,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     if (spec > 0) {
         // behind the slots, all placements again: when they finished the walk,
         // the status round trip below brings the final results with it
-        HIPCK(hipMemcpyAsync(stage, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(stage_spec, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost,
+                             st));
         if (want_raw)
-            HIPCK(hipMemcpyAsync(stage + P, ctx->out_cost_i.p, (size_t)P * 4, hipMemcpyDeviceToHost,
-                                 st));
+            HIPCK(hipMemcpyAsync(stage_spec + P, ctx->out_cost_i.p, (size_t)P * 4,
+                                 hipMemcpyDeviceToHost, st));
     }
     hipEvent_t t1 = nullptr;
     // status words in one copy: halt[0..2] = halt word, slot resumes, commit
@@ -1795,8 +1813,10 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         return wait_event(ctx, t1);
     };
     int unsched = 0;
-    auto unpack = [&](int lo, int hi) {
-        std::memcpy(node_out + lo, stage + lo, (size_t)(hi - lo) * 4);
+    // decode pods [lo, hi) from a staging area (placements, then raw keys)
+    auto unpack = [&](int lo, int hi, const int32_t *from) {
+        const uint32_t *raw = reinterpret_cast<const uint32_t *>(from + P);
+        std::memcpy(node_out + lo, from + lo, (size_t)(hi - lo) * 4);
         for (int i = lo; i < hi; ++i) {
             const bool none = node_out[i] < 0;
             unsched += none;
@@ -1814,16 +1834,17 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     t1 = tm.mark(st);
     for (const Landed &l : landed) {
         OK(wait_event(ctx, l.ev));
-        unpack(l.lo, l.hi);
+        unpack(l.lo, l.hi, stage);
     }
     OK(wait_event(ctx, t1));  // t1 follows everything on st (the status copies)
     int checks = 0;
     if (spec > 0 && hs[0] < 0 && hs[1] > 0) {
         // speculative slots finished a walk that had halted: the per-chunk
         // copies behind the commits predate them; the full copy behind the
-        // slots (same round trip) holds the final placements
+        // slots (same round trip, its own staging area) holds the final
+        // placements
         unsched = 0;
-        unpack(0, P);
+        unpack(0, P, stage_spec);
     }
     while (hs[0] >= 0) {
         // still halted after the pipeline: more gathered slots, checked in batches
@@ -1834,7 +1855,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         OK(fetch());
         if (hs[0] < 0) {
             unsched = 0;
-            unpack(0, P);
+            unpack(0, P, stage);
         }
     }
     tm.span(T_TOTAL, t0, t1);
@@ -2036,77 +2057,157 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     if (ctx->B > 1 && world > 1)
         return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");
     destroy_comms(ctx);
-    ctx->rank = rank;
-    ctx->world = world;
-    ctx->virtual_shard = false;
-    ctx->rehearse = 0;
+    // on any failure below the context keeps its previous geometry (a context
+    // left at world > 1 without communicators would place from its own shard)
+    int32_t eff_world = world, rehearse = 0;
     if (ctx->opt_rehearse_world > 1 && world == 1) {
         // diagnostic (NAS_OPT_REHEARSE_WORLD): one rank of a G-GPU pass
-        ctx->rehearse = ctx->opt_rehearse_world;
-        ctx->world = ctx->rehearse;
+        rehearse = ctx->opt_rehearse_world;
+        eff_world = rehearse;
     }
     ncclUniqueId uid;
     std::memcpy(&uid, id, 128);
-    // The communicators are built on a helper thread under the context's
-    // NAS_OPT_COMM_TIMEOUT_MS deadline: ncclCommInitRank and ncclCommSplit
-    // block until every rank has joined, so a rank whose peers never arrive
-    // (a failed launch, an unreachable bootstrap address) would otherwise hang
-    // here with no way out.  On expiry the call returns NAS_ERR_COMM and the
-    // helper is abandoned; should it still finish, it destroys what it built.
-    // (Blocking communicators are kept: non-blocking ones would make every
-    // collective of the pass return ncclInProgress.)
+    // ncclCommInitRank waits in RCCL's bootstrap until every rank has joined,
+    // in the calling thread (RCCL 2.27, blocking or not), so a rank whose
+    // peers never arrive would block forever.  The communicators are built
+    // on a helper thread: a NON-blocking root (config.blocking = 0), whose
+    // handle RCCL publishes as soon as it exists, and three BLOCKING
+    // children split from it (one per stream that issues collectives:
+    // scoring stream 1, scoring stream 2, commit stream -- each keeps its own
+    // issue order on every rank).  This thread waits under
+    // NAS_OPT_COMM_TIMEOUT_MS; on expiry it aborts the published root, which
+    // ends the helper's bootstrap wait (measured: the helper returns ~2.5 s
+    // after the abort), joins the helper and returns NAS_ERR_COMM -- no
+    // thread of this call outlives it, so a host may retry.
     struct Init {
         std::mutex mu;
         std::condition_variable cv;
         bool done = false, abandoned = false;
+        ncclComm_t root = nullptr;  // written by RCCL (from the helper) once it exists
+        ncclComm_t kids[3] = {nullptr, nullptr, nullptr};
+        bool root_aborted = false;
         ncclResult_t r = ncclSuccess;
-        const char *what = "";
-        ncclComm_t comm = nullptr, comm2 = nullptr, comm_c = nullptr;
+        std::string what;
     };
     auto st = std::make_shared<Init>();
     const int dev = ctx->device;
-    std::thread([st, dev, uid, rank, world]() mutable {
-        ncclComm_t c = nullptr, c2 = nullptr, cc = nullptr;
-        const char *what = "ncclCommInitRank";
+    std::thread helper([st, dev, uid, rank, world]() mutable {
+        using clk = std::chrono::steady_clock;
+        (void)clk::now();
+        auto abandoned = [&] {
+            std::lock_guard<std::mutex> g(st->mu);
+            return st->abandoned;
+        };
+        // poll a communicator of this call until its pending work is done
+        auto settle = [&](ncclComm_t c) -> ncclResult_t {
+            for (;;) {
+                ncclResult_t a = ncclInProgress;
+                const ncclResult_t q = ncclCommGetAsyncError(c, &a);
+                if (q != ncclSuccess) return q;
+                if (a != ncclInProgress) return a;
+                if (abandoned()) return ncclInvalidUsage;
+                std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+        };
         ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
-        if (r == ncclSuccess) r = ncclCommInitRank(&c, world, uid, rank);
-        // one communicator per stream that issues collectives (second scoring
-        // stream, commit stream): each keeps its own issue order on every rank
+        std::string what = "hipSetDevice";
+        ncclComm_t kids[3] = {nullptr, nullptr, nullptr};
         if (r == ncclSuccess) {
+            what = "ncclCommInitRankConfig";
+            ncclConfig_t rc = NCCL_CONFIG_INITIALIZER;
+            rc.blocking = 0;
+            r = ncclCommInitRankConfig(&st->root, world, uid, rank, &rc);
+            ncclComm_t root = __atomic_load_n(&st->root, __ATOMIC_ACQUIRE);
+            if (r == ncclInProgress && root) r = settle(root);
+            if (r == ncclSuccess && !root) r = ncclInternalError;
+        }
+        for (int i = 0; i < 3 && r == ncclSuccess && !abandoned(); ++i) {
             what = "ncclCommSplit";
-            r = ncclCommSplit(c, 0, rank, &c2, nullptr);
-            if (r == ncclSuccess) r = ncclCommSplit(c, 0, rank, &cc, nullptr);
+            ncclConfig_t kc = NCCL_CONFIG_INITIALIZER;
+            kc.blocking = 1;
+            ncclComm_t root = __atomic_load_n(&st->root, __ATOMIC_ACQUIRE);
+            r = ncclCommSplit(root, 0, rank, &kids[i], &kc);
+            // a split of a non-blocking parent may complete in RCCL's async
+            // job, which stores the child handle when it is done
+            while (r == ncclInProgress && !__atomic_load_n(&kids[i], __ATOMIC_ACQUIRE)) {
+                ncclResult_t a = ncclInProgress;
+                const ncclResult_t q = ncclCommGetAsyncError(root, &a);
+                if (q != ncclSuccess || (a != ncclSuccess && a != ncclInProgress)) {
+                    r = q != ncclSuccess ? q : a;
+                    break;
+                }
+                if (abandoned()) {
+                    r = ncclInvalidUsage;
+                    break;
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+            if (r == ncclInProgress || r == ncclSuccess) {
+                ncclComm_t k = __atomic_load_n(&kids[i], __ATOMIC_ACQUIRE);
+                r = k ? settle(k) : ncclInternalError;
+                if (r == ncclSuccess) r = settle(root);
+            }
         }
         std::lock_guard<std::mutex> g(st->mu);
-        if (st->abandoned || r != ncclSuccess) {  // abort: local, no peer handshake
-            for (ncclComm_t x : {cc, c2, c})
-                if (x) (void)ncclCommAbort(x);
-            c = c2 = cc = nullptr;
+        if (r == ncclSuccess && st->abandoned) r = ncclInvalidUsage;
+        if (r != ncclSuccess) {  // abort: local, no peer handshake
+            for (ncclComm_t &k : kids)
+                if (k) (void)ncclCommAbort(k), k = nullptr;
+            if (st->root && !st->root_aborted) (void)ncclCommAbort(st->root);
+            st->root = nullptr;
         }
+        for (int i = 0; i < 3; ++i) st->kids[i] = kids[i];
         st->r = r;
         st->what = what;
-        st->comm = c, st->comm2 = c2, st->comm_c = cc;
         st->done = true;
         st->cv.notify_all();
-    }).detach();
+    });
     std::unique_lock<std::mutex> lk(st->mu);
+    bool expired = false;
     if (ctx->opt_comm_timeout_ms > 0) {
-        if (!st->cv.wait_for(lk, std::chrono::milliseconds(ctx->opt_comm_timeout_ms),
-                             [&] { return st->done; })) {
+        const auto limit = std::chrono::milliseconds(ctx->opt_comm_timeout_ms);
+        expired = !st->cv.wait_for(lk, limit, [&] { return st->done; });
+        if (expired) {
+            // the root's handle appears ~1 s into the init: wait for it (or for
+            // the helper to finish) a bounded while, then abort it
             st->abandoned = true;
-            return nas::fail(ctx, NAS_ERR_COMM,
-                             "nas_comm_init: the communicators were not built within " +
-                                 std::to_string(ctx->opt_comm_timeout_ms) +
-                                 " ms (NAS_OPT_COMM_TIMEOUT_MS): a rank did not join");
+            const auto grace = std::chrono::steady_clock::now() + std::chrono::seconds(30);
+            while (!st->done && !__atomic_load_n(&st->root, __ATOMIC_ACQUIRE) &&
+                   std::chrono::steady_clock::now() < grace)
+                st->cv.wait_for(lk, std::chrono::milliseconds(20));
+            ncclComm_t root = __atomic_load_n(&st->root, __ATOMIC_ACQUIRE);
+            if (!st->done && root) {
+                st->root_aborted = true;
+                lk.unlock();
+                (void)ncclCommAbort(root);  // ends the helper's bootstrap wait
+                lk.lock();
+            }
+            st->cv.wait_until(lk, grace, [&] { return st->done; });
         }
     } else {
         st->cv.wait(lk, [&] { return st->done; });
     }
+    const bool finished = st->done;
+    lk.unlock();
+    if (finished) helper.join();
+    else helper.detach();  // (the abort did not release it within 30 s)
+    if (expired)
+        return nas::fail(ctx, NAS_ERR_COMM,
+                         "nas_comm_init: the communicators did not complete within " +
+                             std::to_string(ctx->opt_comm_timeout_ms) +
+                             " ms (NAS_OPT_COMM_TIMEOUT_MS): a rank did not join; "
+                             "communicators aborted" +
+                             (finished ? "" : " (helper thread still blocked in RCCL)"));
     if (st->r != ncclSuccess)
-        return nas::fail(ctx, NAS_ERR_COMM, std::string(st->what) + ": " + ncclGetErrorString(st->r));
-    ctx->comm = reinterpret_cast<ncclComm *>(st->comm);
-    ctx->comm2 = reinterpret_cast<ncclComm *>(st->comm2);
-    ctx->comm_c = reinterpret_cast<ncclComm *>(st->comm_c);
+        return nas::fail(ctx, NAS_ERR_COMM, st->what + ": " + ncclGetErrorString(st->r));
+    ctx->rank = rank;
+    ctx->world = eff_world;
+    ctx->rehearse = rehearse;
+    ctx->virtual_shard = false;
+    ctx->comm_root = reinterpret_cast<ncclComm *>(st->root);
+    ctx->comm = reinterpret_cast<ncclComm *>(st->kids[0]);
+    ctx->comm2 = reinterpret_cast<ncclComm *>(st->kids[1]);
+    ctx->comm_c = reinterpret_cast<ncclComm *>(st->kids[2]);
     return NAS_OK;
 }
 

@@ -52,6 +52,19 @@ constexpr uint64_t KEY_INVALID = ~0ull;
 // row-major copy of this rank's latency columns (Lr[m][i] = L[m][Nloc0 + i],
 // row stride Mp).  row_pod maps a gathered view's rows to pods (nullptr:
 // row = pod); rows >= *row_count of a view are never read.
+// The cost kernel's fused fit (k_cost.hip; every launch over a main pod range,
+// i.e. not a rescore window): the capacity the scoring reads (live `cap`, or
+// `cap_snap` beside the L2 commit) and the requests, read by the cost
+// workgroups themselves instead of a k_fit mask (batches: cluster cb at
+// cap + cb*3*N, req + cb*3*Pp)
+struct FitSrc {
+    const int32_t *cap = nullptr;  // [3][N]
+    const int32_t *req = nullptr;  // [3][Pp] (row stride = the launch's Pp)
+    int N = 0;                     // row stride of cap
+    int n0 = 0;                    // first node of this shard
+    int nloc = 0;                  // valid local nodes
+};
+
 struct Ovf {
     const int32_t *ptr = nullptr;  // [B * Pp + 1] absolute offsets (nullptr: no entries)
     const int32_t *m = nullptr;
@@ -149,6 +162,9 @@ struct nas_ctx {
     ncclComm *comm = nullptr;    // scoring chunks on `stream` and host-side rescores
     ncclComm *comm2 = nullptr;   // scoring chunks on `stream2`
     ncclComm *comm_c = nullptr;  // rescore slots on `stream_commit`
+    // the non-blocking communicator the three above are split from (nas_comm_init
+    // polls it under a deadline and can abort it); it issues no collectives
+    ncclComm *comm_root = nullptr;
     int32_t rank = 0, world = 1;
     // diagnostic (NAS_REHEARSE_WORLD=G with a one-rank communicator): shard
     // geometry of rank 0 of G, the other G-1 ranks' lists stood in for by
@@ -232,7 +248,8 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base,
                             const Dyn *dyn = nullptr, int batch = 1, const Ovf *ovf = nullptr,
-                            const int32_t *rowmap = nullptr, bool wide = false);
+                            const int32_t *rowmap = nullptr, bool wide = false,
+                            const FitSrc *fit = nullptr);
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,

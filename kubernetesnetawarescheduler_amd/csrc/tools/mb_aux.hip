@@ -66,10 +66,11 @@ int main(int argc, char **argv) {
     int zero = 0;
     const int *nodyn = nullptr;
     Ovf noovf{};
+    FitSrc nofit{};  // (the mask path; FUSE variants are not benchmarked here)
     void *args[] = {&lt, &wa, (void *)&Kp, (void *)&n_mt, (void *)&n_nt, &zero, (void *)&Pp, &mk,
-                    &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf, &nodyn};
+                    &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf, &nodyn, &nofit};
     void *argsb[] = {&ltb, &wab, (void *)&Kb2, (void *)&n_mt, (void *)&n_nt, &zero, (void *)&Pp, &mk,
-                     &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf, &nodyn};
+                     &pa, &pb, &zero, &nodyn, &zero, &nodyn, &noovf, &nodyn, &nofit};
     const char *sel = argc > 4 ? argv[4] : nullptr;  // substring filter on variant names
     for (int r = 0; r < reps; ++r)
         for (const V &v : vars) {

@@ -18,11 +18,27 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int BM = 256, BKB = 128;
 
-template <int NWP, bool DB>
+template <int NI>
+__device__ __forceinline__ void rd(const unsigned char *As, const unsigned char *Bs, int kk, int fh,
+                                   int fr, int wm, int wn, v4i *ra, v4i *rb) {
+    const int c = kk * 2 + fh;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+        const int rw = wm * 128 + mi * 32 + fr;
+        ra[mi] = *reinterpret_cast<const v4i *>(As + rw * BKB + ((c ^ ((rw >> 1) & 7)) << 4));
+    }
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni) {
+        const int rw = wn * 32 * NI + ni * 32 + fr;
+        rb[ni] = *reinterpret_cast<const v4i *>(Bs + rw * BKB + ((c ^ ((rw >> 1) & 7)) << 4));
+    }
+}
+
+template <int NWP, bool DB, int NI>
 __global__ void __launch_bounds__(128 * NWP, 1)
 k_wide(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
        int n_mt, int n_nt) {
-    constexpr int NW = 2 * NWP, BN = 64 * NWP;
+    constexpr int NW = 2 * NWP, BN = 32 * NI * NWP;
     constexpr int STAGE = (BM + BN) * BKB, PIECES = (BM + BN) / 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int nwg = n_mt * n_nt, b = blockIdx.x;
@@ -50,30 +66,20 @@ k_wide(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ W
                                              16, 0, 0);
         }
     };
-    v16i acc[4][2];
+    v16i acc[4][4];  // (only [..NI) used: a dependent bound here loses the host stubs, hipcc 7.2)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = v16i{};
+        for (int j = 0; j < NI; ++j) acc[i][j] = v16i{};
     const int fr = lane & 31, fh = lane >> 5;
     auto compute = [&](int buf) {
         const unsigned char *As = lds + buf * STAGE;
         const unsigned char *Bs = As + BM * BKB;
-        auto read = [&](int kk, v4i (&ra)[4], v4i (&rb)[2]) {
-            const int c = kk * 2 + fh;
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int rw = wm * 128 + mi * 32 + fr;
-                ra[mi] = *reinterpret_cast<const v4i *>(As + rw * BKB + ((c ^ ((rw >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int ni = 0; ni < 2; ++ni) {
-                const int rw = wn * 64 + ni * 32 + fr;
-                rb[ni] = *reinterpret_cast<const v4i *>(Bs + rw * BKB + ((c ^ ((rw >> 1) & 7)) << 4));
-            }
+        auto read = [&](int kk, v4i *ra, v4i *rb) {
+            rd<NI>(As, Bs, kk, fh, fr, wm, wn, ra, rb);
         };
         if constexpr (DB) {
-            v4i a[2][4], bb[2][2];
+            v4i a[2][4], bb[2][NI];
             read(0, a[0], bb[0]);
 #pragma unroll
             for (int kk = 0; kk < BKB / 32; ++kk) {
@@ -81,19 +87,19 @@ k_wide(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ W
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                    for (int ni = 0; ni < 2; ++ni)
+                    for (int ni = 0; ni < NI; ++ni)
                         acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kk & 1][mi], bb[kk & 1][ni],
                                                                             acc[mi][ni], 0, 0, 0);
             }
         } else {
 #pragma unroll
             for (int kk = 0; kk < BKB / 32; ++kk) {
-                v4i a[4], bb[2];
+                v4i a[4], bb[NI];
                 read(kk, a, bb);
 #pragma unroll
                 for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-                    for (int ni = 0; ni < 2; ++ni)
+                    for (int ni = 0; ni < NI; ++ni)
                         acc[mi][ni] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[mi], bb[ni], acc[mi][ni], 0, 0, 0);
             }
         }
@@ -112,23 +118,23 @@ k_wide(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ W
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) asm volatile("" ::"v"(acc[mi][ni]));
+        for (int ni = 0; ni < NI; ++ni) asm volatile("" ::"v"(acc[mi][ni]));
 }
 
-template <int NWP, bool DB>
+template <int NWP, bool DB, int NI>
 void run(const char *name, const unsigned char *Lt, const unsigned char *WA, int Kp, int Mp, int P,
          int reps) {
-    constexpr int BN = 64 * NWP;
+    constexpr int BN = 32 * NI * NWP;
     const int Pp = (P + BN - 1) / BN * BN;
     const int n_mt = Mp / BM, n_nt = Pp / BN;
     const int lds = 2 * (BM + BN) * BKB;
-    CK(hipFuncSetAttribute((const void *)&k_wide<NWP, DB>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    CK(hipFuncSetAttribute((const void *)&k_wide<NWP, DB, NI>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     for (int r = 0; r <= reps; ++r) {
         CK(hipEventRecord(a));
-        k_wide<NWP, DB><<<n_mt * n_nt, 128 * NWP, lds>>>(Lt, WA, Kp, n_mt, n_nt);
+        k_wide<NWP, DB, NI><<<n_mt * n_nt, 128 * NWP, lds>>>(Lt, WA, Kp, n_mt, n_nt);
         CK(hipGetLastError());
         CK(hipEventRecord(b));
         CK(hipEventSynchronize(b));
@@ -152,10 +158,13 @@ int main(int argc, char **argv) {
     CK(hipMemcpy(Lt, h.data(), (size_t)Mp * Kp, hipMemcpyHostToDevice));
     const auto *lt = (const unsigned char *)Lt, *wa = (const unsigned char *)WA;
     for (int i = 0; i < 2; ++i) {
-        run<4, true>("w256x256/8w/db", lt, wa, Kp, Mp, P, reps);
-        run<6, false>("w256x384/12w/sb", lt, wa, Kp, Mp, P, reps);
-        run<6, true>("w256x384/12w/db", lt, wa, Kp, Mp, P, reps);
-        run<4, false>("w256x256/8w/sb", lt, wa, Kp, Mp, P, reps);
+        run<4, true, 2>("w256x256/8w/db", lt, wa, Kp, Mp, P, reps);
+        run<6, false, 2>("w256x384/12w/sb", lt, wa, Kp, Mp, P, reps);
+        run<6, true, 2>("w256x384/12w/db", lt, wa, Kp, Mp, P, reps);
+        run<4, false, 2>("w256x256/8w/sb", lt, wa, Kp, Mp, P, reps);
+        run<4, false, 3>("w256x384/8w128x96/sb", lt, wa, Kp, Mp, P, reps);
+        run<4, true, 3>("w256x384/8w128x96/db", lt, wa, Kp, Mp, P, reps);
+        run<2, false, 4>("w256x256/4w128x128/sb", lt, wa, Kp, Mp, P, reps);
     }
     return 0;
 }

@@ -293,7 +293,12 @@ class Engine:
                                                 P, n, pn.shape[0]))
         self.n_pods, self.n_nodes, self.dtype = P, n, "i8" if dtype in ("i8", "i32") else dtype
 
-    def filter(self):
+    def filter(self, want_mask=True):
+        """nas_filter: the fit mask [chunk][pod] (bit j of word (c, p) = pod p
+        fits node 64c + j); want_mask=False runs the kernel alone (timing)."""
+        if not want_mask:
+            self._ck(self._L.nas_filter(self._h, None))
+            return None
         chunks = (self.n_nodes + 63) // 64
         mask = np.zeros((chunks, self.n_pods), np.uint64)
         self._ck(self._L.nas_filter(self._h, ptr(mask)))

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -176,8 +177,12 @@ int nas_host_snapshot_from_bodies(int32_t n, const char *const *bodies, const si
         return NAS_ERR_ARG;
     for (int32_t i = 0; i < n; ++i)
         if ((!bodies[i] && body_len[i]) || !names[i]) return NAS_ERR_ARG;
+    // any exception stays inside its node: a worker thread must not reach
+    // std::terminate, and nothing may cross the extern "C" boundary
+    std::atomic<bool> other_error{false};
     auto one = [&](int32_t i) {
         const std::string_view b(bodies[i] ? bodies[i] : "", body_len[i]);
+        int st = NAS_OK;
         try {
             const double c = get_current_cpu_usage(b);
             const double m = get_occupied_memory_percentage(b);
@@ -185,28 +190,36 @@ int nas_host_snapshot_from_bodies(int32_t n, const char *const *bodies, const si
             const int64_t t = get_network_packets_sent(b, names[i]);
             const int64_t d = get_disk_io_now(b, names[i]);
             cpu[i] = c, mem[i] = m, rx[i] = r, tx[i] = t, disk[i] = d;
-            status[i] = NAS_OK;
         } catch (const GoPanic &) {
+            st = NAS_HOST_PANIC;
+        } catch (...) {  // bad_alloc and the like: not a reference behaviour
+            st = NAS_ERR_STATE;
+            other_error.store(true, std::memory_order_relaxed);
+        }
+        if (st != NAS_OK) {
             cpu[i] = mem[i] = 0;
             rx[i] = tx[i] = disk[i] = 0;
-            status[i] = NAS_HOST_PANIC;
         }
+        status[i] = st;
     };
     int w = threads > 0 ? threads : (int)std::max(1u, std::thread::hardware_concurrency());
     w = std::max(1, std::min<int>(w, n / 64 + 1));  // >= 64 nodes per worker
-    if (w == 1) {
-        for (int32_t i = 0; i < n; ++i) one(i);
-        return NAS_OK;
-    }
+    auto range = [&](int k) {
+        const int32_t lo = (int32_t)((int64_t)n * k / w), hi = (int32_t)((int64_t)n * (k + 1) / w);
+        for (int32_t i = lo; i < hi; ++i) one(i);
+    };
     std::vector<std::thread> pool;
-    pool.reserve(w);
-    for (int k = 0; k < w; ++k)
-        pool.emplace_back([&, k] {
-            const int32_t lo = (int32_t)((int64_t)n * k / w), hi = (int32_t)((int64_t)n * (k + 1) / w);
-            for (int32_t i = lo; i < hi; ++i) one(i);
-        });
+    int started = 0;
+    if (w > 1) {
+        try {
+            pool.reserve(w);
+            for (; started < w; ++started) pool.emplace_back(range, started);
+        } catch (...) {  // could not start a worker: this thread does the rest
+        }
+    }
+    for (int k = started; k < w; ++k) range(k);
     for (auto &t : pool) t.join();
-    return NAS_OK;
+    return other_error.load() ? NAS_ERR_STATE : NAS_OK;
 }
 
 int nas_host_iperf_receiver(const char *json, size_t n, double *receiver_bps, double *sender_bps,

@@ -75,3 +75,32 @@ def test_c2_workload_equals_oracle():
     want, wcost, wfree = oracle.place(WA, c["L"], c["req"], c["free"], "i8")
     assert node.tolist() == want.tolist() and score.tolist() == wcost.tolist()
     assert (cap == wfree).all()
+
+
+@pytest.mark.parametrize("B", [300, 1100])
+def test_large_batch_of_tiny_clusters(B):
+    """More clusters than the first pinned page of status words holds
+    (4096 B / 16 B = 256): the staged placements must not be overwritten by
+    the status round trip."""
+    rng = np.random.default_rng(B)
+    P, N = 40, 64
+    cs = []
+    for b in range(B):
+        WA, L, free, req = cluster(rng, P, N, lo=0, hi=40, cap_scale=0.05 + 0.002 * (b % 50))
+        if b % 3 == 0:
+            WA[:, rng.choice(N, 3, replace=False)] = 127  # crowding: stops, rescores
+        cs.append((WA, L, free, req))
+    with Engine(0) as e:
+        e.set_batch(B)
+        e.upload_latency(np.stack([c[1] for c in cs]), "i8")
+        e.upload_capacity(np.stack([c[2] for c in cs]))
+        e.upload_pods(np.stack([c[3] for c in cs]))
+        e.upload_traffic(np.stack([c[0] for c in cs]), "i8")
+        node, cost, score = e.place()
+        cap = e.get_capacity()
+    for b, (WA, L, free, req) in enumerate(cs):
+        want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
+        assert node[b].tolist() == want.tolist(), b
+        assert score[b].tolist() == wcost.tolist(), b
+        assert cost[b].tolist() == [float(x) for x in wcost], b
+        assert (cap[b] == wfree).all(), b

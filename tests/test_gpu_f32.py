@@ -83,7 +83,12 @@ def _gaps_at_turn(node, cost, req, free):
         c = np.where(fits, cost[p], np.inf)
         if np.isfinite(c).sum() >= 2:
             a, b = np.partition(c, 1)[:2]
-            gaps[p] = (b - a) / abs(a)
+            # relative to the larger magnitude, so a zero best cost divides
+            # nothing by zero; two exact zeros (a pod with no traffic: every
+            # product is 0 on the GPU too) are no rounding ambiguity -- the
+            # node index decides them on both sides -- so they are not a tie
+            scale = max(abs(a), abs(b))
+            gaps[p] = (b - a) / scale if scale > 0 else np.inf
         if node[p] >= 0:
             cap[node[p]] -= req[p]
     return gaps
