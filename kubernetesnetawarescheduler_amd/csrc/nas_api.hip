@@ -395,6 +395,36 @@ int check_extended(nas_ctx *ctx) {
     return NAS_OK;
 }
 
+void abort_comms(nas_ctx *ctx);
+
+// The communicators are NON-blocking (nas_comm_init): a collective may return
+// ncclInProgress while RCCL finishes enqueueing it (e.g. a lazy connection
+// set-up); poll the communicator until it is enqueued, under the same
+// NAS_OPT_COMM_TIMEOUT_MS deadline as the waits (abort + poison on expiry).
+int nccl_enqueued(nas_ctx *ctx, ncclComm *cm, ncclResult_t r, const char *what) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    while (r == ncclInProgress) {
+        ncclResult_t a = ncclInProgress;
+        const ncclResult_t q = ncclCommGetAsyncError(reinterpret_cast<ncclComm_t>(cm), &a);
+        r = q != ncclSuccess ? q : a;
+        if (r != ncclInProgress) break;
+        if (ctx->opt_comm_timeout_ms > 0 &&
+            clk::now() - t0 > std::chrono::milliseconds(ctx->opt_comm_timeout_ms)) {
+            abort_comms(ctx);
+            return nas::fail(ctx, NAS_ERR_COMM,
+                             std::string(what) + " was not enqueued within " +
+                                 std::to_string(ctx->opt_comm_timeout_ms) +
+                                 " ms (NAS_OPT_COMM_TIMEOUT_MS): communicators aborted, "
+                                 "context poisoned");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if (r != ncclSuccess)
+        return nas::fail(ctx, NAS_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
+    return NAS_OK;
+}
+
 // all-gather each rank's per-pod lists (keys [np][KC] + bounds [np]) into
 // gk [world][np][KC] / gb [world][np] on `st` over communicator `cm`
 int exchange(nas_ctx *ctx, ncclComm *cm, hipStream_t st, const uint64_t *keys,
@@ -405,8 +435,7 @@ int exchange(nas_ctx *ctx, ncclComm *cm, hipStream_t st, const uint64_t *keys,
     if (r == ncclSuccess) r = ncclAllGather(bounds, gb, np, ncclUint64, comm, st);
     ncclResult_t r2 = ncclGroupEnd();
     if (r == ncclSuccess) r = r2;
-    if (r != ncclSuccess)
-        return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+    OK(nccl_enqueued(ctx, cm, r, "ncclAllGather"));
     if (ctx->rehearse > 1) {
         HIPCK(nas::launch_rehearse_replicate(st, gk, np * KC, ctx->rehearse, ctx->N));
         HIPCK(nas::launch_rehearse_replicate(st, gb, np, ctx->rehearse, ctx->N));
@@ -458,8 +487,7 @@ int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, ncc
                                 n_lists, (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, xs,
                                 xs + (size_t)np * KC, pr0));
         ncclResult_t r = ncclAllGather(xs, gx, seg, ncclUint64, reinterpret_cast<ncclComm_t>(cm), st);
-        if (r != ncclSuccess)
-            return nas::fail(ctx, NAS_ERR_COMM, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        OK(nccl_enqueued(ctx, cm, r, "ncclAllGather"));
         if (ctx->rehearse > 1)
             HIPCK(nas::launch_rehearse_replicate(st, gx, seg, ctx->rehearse, ctx->N));
         HIPCK(nas::launch_merge(st, gx, gx + (size_t)np * KC, ctx->world, (int64_t)seg,
@@ -820,7 +848,14 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     const int mode = big > 32 ? 2 : 0;
     const int left = (ctx->P - lo + nas::COST_BN - 1) / nas::COST_BN;  // pod tiles left
     int tiles = c == 0 ? 32 : big;
-    if (tile_pods(ctx) != nas::COST_BN) tiles = CHUNK_TILES_WIDE;  // (one cluster, G = 1)
+    // (one cluster, G = 1) the wide tile's chunks: the first chunk of the
+    // second scoring stream is half as long, so the two streams' chunk
+    // boundaries stay half a chunk apart -- a stream's next chunk waits for
+    // its previous one to complete, and while that drains its last round the
+    // other stream still has undispatched workgroups to fill the CUs (with
+    // equal chunks both streams drained together: ~20 us of idle CUs per
+    // chunk pair in the C3 pass timeline)
+    if (tile_pods(ctx) != nas::COST_BN) tiles = c == 1 ? CHUNK_TILES_WIDE / 2 : CHUNK_TILES_WIDE;
     // a pass whose pods fit one big chunk (C2: 40 pod tiles on 4 node tiles)
     // is one chunk: pipelining its short tail would save less than the
     // cross-stream hops and launches it adds (device time 0.96 -> 0.92 ms, C2)
@@ -888,8 +923,22 @@ float decode_cost(uint32_t raw, int dtype) {
 }
 
 void destroy_comms(nas_ctx *ctx) {
+    // non-blocking communicators: finalize (flush, in RCCL's async job), poll
+    // it to completion, then destroy; a finalize that fails or does not
+    // finish within 10 s is aborted instead (local, no peer handshake)
     for (ncclComm **c : {&ctx->comm, &ctx->comm2, &ctx->comm_c}) {
-        if (*c) (void)ncclCommDestroy(reinterpret_cast<ncclComm_t>(*c));
+        if (!*c) continue;
+        auto comm = reinterpret_cast<ncclComm_t>(*c);
+        ncclResult_t r = ncclCommFinalize(comm);
+        const auto limit = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+        while (r == ncclInProgress && std::chrono::steady_clock::now() < limit) {
+            ncclResult_t a = ncclInProgress;
+            const ncclResult_t q = ncclCommGetAsyncError(comm, &a);
+            r = q != ncclSuccess ? q : a;
+            if (r == ncclInProgress) std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+        if (r == ncclSuccess) (void)ncclCommDestroy(comm);
+        else (void)ncclCommAbort(comm);
         *c = nullptr;
     }
     // the non-blocking root issued no collectives and owns nothing the
@@ -1202,8 +1251,7 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
         b = tm.mark();  // vote_ms: the slice's HBM pass alone
         ncclResult_t r = ncclAllGather(ctx->vote_part.p, ctx->vote_gather.p, rb, ncclUint8,
                                        reinterpret_cast<ncclComm_t>(ctx->comm), ctx->stream);
-        if (r != ncclSuccess)
-            return nas::fail(ctx, NAS_ERR_COMM, std::string("vote all-gather: ") + ncclGetErrorString(r));
+        OK(nccl_enqueued(ctx, ctx->comm, r, "vote all-gather"));
         HIPCK(nas::launch_vote_merge(ctx->stream, ctx, ctx->vote_gather.as<nas_vote_partial>(),
                                      ranks, Sused, ctx->snap_best.as<int32_t>(),
                                      ctx->snap_win.as<int32_t>()));
@@ -2070,30 +2118,30 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     // ncclCommInitRank waits in RCCL's bootstrap until every rank has joined,
     // in the calling thread (RCCL 2.27, blocking or not), so a rank whose
     // peers never arrive would block forever.  The communicators are built
-    // on a helper thread: a NON-blocking root (config.blocking = 0), whose
-    // handle RCCL publishes as soon as it exists, and three BLOCKING
-    // children split from it (one per stream that issues collectives:
-    // scoring stream 1, scoring stream 2, commit stream -- each keeps its own
-    // issue order on every rank).  This thread waits under
-    // NAS_OPT_COMM_TIMEOUT_MS; on expiry it aborts the published root, which
-    // ends the helper's bootstrap wait (measured: the helper returns ~2.5 s
-    // after the abort), joins the helper and returns NAS_ERR_COMM -- no
-    // thread of this call outlives it, so a host may retry.
+    // on a helper thread, all NON-blocking (config.blocking = 0; RCCL 2.26
+    // refuses a blocking child split from a non-blocking root): a root, whose
+    // handle RCCL publishes as soon as it exists, and three children split
+    // from it (one per stream that issues collectives: scoring stream 1,
+    // scoring stream 2, commit stream -- each keeps its own issue order on
+    // every rank), each warmed up by one small all-gather so its connections
+    // exist before the first pass (the pass's collectives then enqueue at
+    // once; nccl_enqueued polls the rare ncclInProgress).  This thread waits
+    // under NAS_OPT_COMM_TIMEOUT_MS; on expiry it aborts every published
+    // communicator, which ends the helper's bootstrap wait (measured: the
+    // helper returns ~2.5 s after the abort), joins the helper and returns
+    // NAS_ERR_COMM -- no thread of this call outlives it, so a host may retry.
     struct Init {
         std::mutex mu;
         std::condition_variable cv;
-        bool done = false, abandoned = false;
-        ncclComm_t root = nullptr;  // written by RCCL (from the helper) once it exists
-        ncclComm_t kids[3] = {nullptr, nullptr, nullptr};
-        bool root_aborted = false;
+        bool done = false, abandoned = false, aborted = false;
+        ncclComm_t root = nullptr;                       // written by RCCL from the helper
+        ncclComm_t kids[3] = {nullptr, nullptr, nullptr};  // likewise
         ncclResult_t r = ncclSuccess;
         std::string what;
     };
     auto st = std::make_shared<Init>();
     const int dev = ctx->device;
     std::thread helper([st, dev, uid, rank, world]() mutable {
-        using clk = std::chrono::steady_clock;
-        (void)clk::now();
         auto abandoned = [&] {
             std::lock_guard<std::mutex> g(st->mu);
             return st->abandoned;
@@ -2109,27 +2157,23 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
                 std::this_thread::sleep_for(std::chrono::microseconds(200));
             }
         };
+        auto load = [](ncclComm_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); };
         ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
         std::string what = "hipSetDevice";
-        ncclComm_t kids[3] = {nullptr, nullptr, nullptr};
         if (r == ncclSuccess) {
             what = "ncclCommInitRankConfig";
             ncclConfig_t rc = NCCL_CONFIG_INITIALIZER;
             rc.blocking = 0;
             r = ncclCommInitRankConfig(&st->root, world, uid, rank, &rc);
-            ncclComm_t root = __atomic_load_n(&st->root, __ATOMIC_ACQUIRE);
-            if (r == ncclInProgress && root) r = settle(root);
-            if (r == ncclSuccess && !root) r = ncclInternalError;
+            if (r == ncclInProgress && load(&st->root)) r = settle(load(&st->root));
+            if (r == ncclSuccess && !load(&st->root)) r = ncclInternalError;
         }
-        for (int i = 0; i < 3 && r == ncclSuccess && !abandoned(); ++i) {
+        for (int i = 0; i < 3 && r == ncclSuccess; ++i) {
             what = "ncclCommSplit";
-            ncclConfig_t kc = NCCL_CONFIG_INITIALIZER;
-            kc.blocking = 1;
-            ncclComm_t root = __atomic_load_n(&st->root, __ATOMIC_ACQUIRE);
-            r = ncclCommSplit(root, 0, rank, &kids[i], &kc);
-            // a split of a non-blocking parent may complete in RCCL's async
-            // job, which stores the child handle when it is done
-            while (r == ncclInProgress && !__atomic_load_n(&kids[i], __ATOMIC_ACQUIRE)) {
+            ncclComm_t root = load(&st->root);
+            r = ncclCommSplit(root, 0, rank, &st->kids[i], nullptr);  // inherits non-blocking
+            // the async split stores the child handle when it is done
+            while (r == ncclInProgress && !load(&st->kids[i])) {
                 ncclResult_t a = ncclInProgress;
                 const ncclResult_t q = ncclCommGetAsyncError(root, &a);
                 if (q != ncclSuccess || (a != ncclSuccess && a != ncclInProgress)) {
@@ -2143,20 +2187,60 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
                 std::this_thread::sleep_for(std::chrono::microseconds(200));
             }
             if (r == ncclInProgress || r == ncclSuccess) {
-                ncclComm_t k = __atomic_load_n(&kids[i], __ATOMIC_ACQUIRE);
+                ncclComm_t k = load(&st->kids[i]);
                 r = k ? settle(k) : ncclInternalError;
                 if (r == ncclSuccess) r = settle(root);
             }
         }
+        if (r == ncclSuccess) {
+            // warm-up: one 8-byte all-gather per child (connections set up now,
+            // inside the deadline, not in the first pass)
+            what = "warm-up all-gather";
+            hipStream_t s = nullptr;
+            void *buf = nullptr;
+            hipEvent_t ev = nullptr;
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+                hipMalloc(&buf, 8 * ((size_t)world + 1)) != hipSuccess ||
+                hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+                r = ncclUnhandledCudaError;
+            for (int i = 0; i < 3 && r == ncclSuccess; ++i) {
+                ncclComm_t k = load(&st->kids[i]);
+                r = ncclAllGather(buf, static_cast<char *>(buf) + 8, 1, ncclUint64, k, s);
+                if (r == ncclInProgress) r = settle(k);
+            }
+            if (r == ncclSuccess && hipEventRecord(ev, s) != hipSuccess) r = ncclUnhandledCudaError;
+            bool drained = r != ncclSuccess;  // (nothing was enqueued on failure)
+            while (r == ncclSuccess && !drained) {
+                const hipError_t q = hipEventQuery(ev);
+                if (q == hipSuccess) drained = true;
+                else if (q != hipErrorNotReady) r = ncclUnhandledCudaError;
+                else if (abandoned()) r = ncclInvalidUsage;
+                else std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+            if (!drained) {
+                // abandoned with collectives in flight: the aborts end them;
+                // give them a bounded while, then leak the scratch
+                for (int i = 0; i < 50000 && hipEventQuery(ev) == hipErrorNotReady; ++i)
+                    std::this_thread::sleep_for(std::chrono::microseconds(200));
+                drained = hipEventQuery(ev) == hipSuccess;
+            }
+            if (drained) {
+                if (ev) (void)hipEventDestroy(ev);
+                if (buf) (void)hipFree(buf);
+                if (s) (void)hipStreamDestroy(s);
+            }
+        }
         std::lock_guard<std::mutex> g(st->mu);
         if (r == ncclSuccess && st->abandoned) r = ncclInvalidUsage;
-        if (r != ncclSuccess) {  // abort: local, no peer handshake
-            for (ncclComm_t &k : kids)
-                if (k) (void)ncclCommAbort(k), k = nullptr;
-            if (st->root && !st->root_aborted) (void)ncclCommAbort(st->root);
+        if (r != ncclSuccess && !st->aborted) {  // abort: local, no peer handshake
+            for (ncclComm_t &k : st->kids)
+                if (k) (void)ncclCommAbort(k);
+            if (st->root) (void)ncclCommAbort(st->root);
+        }
+        if (r != ncclSuccess) {
+            for (ncclComm_t &k : st->kids) k = nullptr;
             st->root = nullptr;
         }
-        for (int i = 0; i < 3; ++i) st->kids[i] = kids[i];
         st->r = r;
         st->what = what;
         st->done = true;
@@ -2169,17 +2253,20 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
         expired = !st->cv.wait_for(lk, limit, [&] { return st->done; });
         if (expired) {
             // the root's handle appears ~1 s into the init: wait for it (or for
-            // the helper to finish) a bounded while, then abort it
+            // the helper to finish) a bounded while, then abort what exists
             st->abandoned = true;
             const auto grace = std::chrono::steady_clock::now() + std::chrono::seconds(30);
             while (!st->done && !__atomic_load_n(&st->root, __ATOMIC_ACQUIRE) &&
                    std::chrono::steady_clock::now() < grace)
                 st->cv.wait_for(lk, std::chrono::milliseconds(20));
-            ncclComm_t root = __atomic_load_n(&st->root, __ATOMIC_ACQUIRE);
-            if (!st->done && root) {
-                st->root_aborted = true;
+            if (!st->done) {
+                ncclComm_t hs[4];
+                for (int i = 0; i < 3; ++i) hs[i] = __atomic_load_n(&st->kids[i], __ATOMIC_ACQUIRE);
+                hs[3] = __atomic_load_n(&st->root, __ATOMIC_ACQUIRE);
+                st->aborted = true;
                 lk.unlock();
-                (void)ncclCommAbort(root);  // ends the helper's bootstrap wait
+                for (ncclComm_t h : hs)  // ends the helper's waits inside RCCL
+                    if (h) (void)ncclCommAbort(h);
                 lk.lock();
             }
             st->cv.wait_until(lk, grace, [&] { return st->done; });
@@ -2190,7 +2277,7 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     const bool finished = st->done;
     lk.unlock();
     if (finished) helper.join();
-    else helper.detach();  // (the abort did not release it within 30 s)
+    else helper.detach();  // (the aborts did not release it within 30 s)
     if (expired)
         return nas::fail(ctx, NAS_ERR_COMM,
                          "nas_comm_init: the communicators did not complete within " +
