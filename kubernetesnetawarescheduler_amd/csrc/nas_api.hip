@@ -2118,10 +2118,11 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     // ncclCommInitRank waits in RCCL's bootstrap until every rank has joined,
     // in the calling thread (RCCL 2.27, blocking or not), so a rank whose
     // peers never arrive would block forever.  The communicators are built
-    // on a helper thread, all NON-blocking (config.blocking = 0; RCCL 2.26
-    // refuses a blocking child split from a non-blocking root): a root, whose
-    // handle RCCL publishes as soon as it exists, and three children split
-    // from it (one per stream that issues collectives: scoring stream 1,
+    // on a helper thread, all NON-blocking (config.blocking = 0): a root,
+    // whose handle RCCL publishes as soon as it exists, and three children
+    // initialised from ids rank 0 broadcasts over the root (no ncclCommSplit:
+    // RCCL 2.26 fails a split of a non-blocking root with an internal error)
+    // (one per stream that issues collectives: scoring stream 1,
     // scoring stream 2, commit stream -- each keeps its own issue order on
     // every rank), each warmed up by one small all-gather so its connections
     // exist before the first pass (the pass's collectives then enqueue at
@@ -2168,67 +2169,93 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
             if (r == ncclInProgress && load(&st->root)) r = settle(load(&st->root));
             if (r == ncclSuccess && !load(&st->root)) r = ncclInternalError;
         }
-        for (int i = 0; i < 3 && r == ncclSuccess; ++i) {
-            what = "ncclCommSplit";
-            ncclComm_t root = load(&st->root);
-            r = ncclCommSplit(root, 0, rank, &st->kids[i], nullptr);  // inherits non-blocking
-            // the async split stores the child handle when it is done
-            while (r == ncclInProgress && !load(&st->kids[i])) {
-                ncclResult_t a = ncclInProgress;
-                const ncclResult_t q = ncclCommGetAsyncError(root, &a);
-                if (q != ncclSuccess || (a != ncclSuccess && a != ncclInProgress)) {
-                    r = q != ncclSuccess ? q : a;
-                    break;
-                }
-                if (abandoned()) {
-                    r = ncclInvalidUsage;
-                    break;
-                }
+        hipStream_t s = nullptr;
+        void *buf = nullptr;
+        hipEvent_t ev = nullptr;
+        // device scratch: 3 child ids (broadcast) and the warm-up all-gathers
+        const size_t scratch = 3 * sizeof(ncclUniqueId) + 8 * ((size_t)world + 1);
+        if (r == ncclSuccess &&
+            (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+             hipMalloc(&buf, scratch) != hipSuccess ||
+             hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess))
+            r = ncclUnhandledCudaError;
+        // wait for everything enqueued on s (polled, so an abandoned init ends)
+        auto drain = [&]() -> ncclResult_t {
+            if (hipEventRecord(ev, s) != hipSuccess) return ncclUnhandledCudaError;
+            for (;;) {
+                const hipError_t q = hipEventQuery(ev);
+                if (q == hipSuccess) return ncclSuccess;
+                if (q != hipErrorNotReady) return ncclUnhandledCudaError;
+                if (abandoned()) return ncclInvalidUsage;
                 std::this_thread::sleep_for(std::chrono::microseconds(200));
             }
-            if (r == ncclInProgress || r == ncclSuccess) {
-                ncclComm_t k = load(&st->kids[i]);
-                r = k ? settle(k) : ncclInternalError;
-                if (r == ncclSuccess) r = settle(root);
+        };
+        bool inflight = false;  // collectives enqueued on s and not yet drained
+        // the three children: rank 0 draws their ids and broadcasts them over
+        // the root, every rank then initialises them as ordinary non-blocking
+        // communicators (ncclCommSplit of a non-blocking root returns
+        // ncclInternalError on torch's RCCL 2.26.6: see the round-3 GPU test log)
+        ncclUniqueId *kid_ids = nullptr;  // pinned: the copies never block the thread
+        const size_t ids_bytes = 3 * sizeof(ncclUniqueId);
+        if (r == ncclSuccess && hipHostMalloc(reinterpret_cast<void **>(&kid_ids), ids_bytes,
+                                              hipHostMallocDefault) != hipSuccess)
+            r = ncclUnhandledCudaError;
+        if (r == ncclSuccess) {
+            what = "child ids";
+            std::memset(kid_ids, 0, ids_bytes);
+            if (rank == 0)
+                for (int i = 0; i < 3 && r == ncclSuccess; ++i) r = ncclGetUniqueId(&kid_ids[i]);
+            if (r == ncclSuccess &&
+                hipMemcpyAsync(buf, kid_ids, ids_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+                r = ncclUnhandledCudaError;
+            if (r == ncclSuccess) {
+                ncclComm_t root = load(&st->root);
+                r = ncclBroadcast(buf, buf, ids_bytes, ncclUint8, 0, root, s);
+                if (r == ncclInProgress) r = settle(root);
+                inflight = r == ncclSuccess;
             }
+            if (r == ncclSuccess &&
+                hipMemcpyAsync(kid_ids, buf, ids_bytes, hipMemcpyDeviceToHost, s) != hipSuccess)
+                r = ncclUnhandledCudaError;
+            if (r == ncclSuccess) r = drain();
+            if (r == ncclSuccess) inflight = false;
+        }
+        for (int i = 0; i < 3 && r == ncclSuccess; ++i) {
+            what = "ncclCommInitRankConfig (child)";
+            ncclConfig_t kc = NCCL_CONFIG_INITIALIZER;
+            kc.blocking = 0;
+            r = ncclCommInitRankConfig(&st->kids[i], world, kid_ids[i], rank, &kc);
+            if (r == ncclInProgress && load(&st->kids[i])) r = settle(load(&st->kids[i]));
+            if (r == ncclSuccess && !load(&st->kids[i])) r = ncclInternalError;
         }
         if (r == ncclSuccess) {
             // warm-up: one 8-byte all-gather per child (connections set up now,
             // inside the deadline, not in the first pass)
             what = "warm-up all-gather";
-            hipStream_t s = nullptr;
-            void *buf = nullptr;
-            hipEvent_t ev = nullptr;
-            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
-                hipMalloc(&buf, 8 * ((size_t)world + 1)) != hipSuccess ||
-                hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
-                r = ncclUnhandledCudaError;
+            char *w = static_cast<char *>(buf) + ids_bytes;
             for (int i = 0; i < 3 && r == ncclSuccess; ++i) {
                 ncclComm_t k = load(&st->kids[i]);
-                r = ncclAllGather(buf, static_cast<char *>(buf) + 8, 1, ncclUint64, k, s);
+                r = ncclAllGather(w, w + 8, 1, ncclUint64, k, s);
                 if (r == ncclInProgress) r = settle(k);
+                inflight = inflight || r == ncclSuccess;
             }
-            if (r == ncclSuccess && hipEventRecord(ev, s) != hipSuccess) r = ncclUnhandledCudaError;
-            bool drained = r != ncclSuccess;  // (nothing was enqueued on failure)
-            while (r == ncclSuccess && !drained) {
-                const hipError_t q = hipEventQuery(ev);
-                if (q == hipSuccess) drained = true;
-                else if (q != hipErrorNotReady) r = ncclUnhandledCudaError;
-                else if (abandoned()) r = ncclInvalidUsage;
-                else std::this_thread::sleep_for(std::chrono::microseconds(200));
-            }
-            if (!drained) {
-                // abandoned with collectives in flight: the aborts end them;
-                // give them a bounded while, then leak the scratch
-                for (int i = 0; i < 50000 && hipEventQuery(ev) == hipErrorNotReady; ++i)
-                    std::this_thread::sleep_for(std::chrono::microseconds(200));
-                drained = hipEventQuery(ev) == hipSuccess;
-            }
-            if (drained) {
-                if (ev) (void)hipEventDestroy(ev);
-                if (buf) (void)hipFree(buf);
-                if (s) (void)hipStreamDestroy(s);
-            }
+            if (r == ncclSuccess) r = drain();
+            if (r == ncclSuccess) inflight = false;
+        }
+        bool drained = !inflight;
+        if (!drained && ev) {
+            // abandoned with collectives in flight: the aborts end them;
+            // give them a bounded while, then leak the scratch
+            (void)hipEventRecord(ev, s);
+            for (int i = 0; i < 50000 && hipEventQuery(ev) == hipErrorNotReady; ++i)
+                std::this_thread::sleep_for(std::chrono::microseconds(200));
+            drained = hipEventQuery(ev) == hipSuccess;
+        }
+        if (drained) {
+            if (ev) (void)hipEventDestroy(ev);
+            if (buf) (void)hipFree(buf);
+            if (kid_ids) (void)hipHostFree(kid_ids);
+            if (s) (void)hipStreamDestroy(s);
         }
         std::lock_guard<std::mutex> g(st->mu);
         if (r == ncclSuccess && st->abandoned) r = ncclInvalidUsage;

@@ -99,3 +99,24 @@ def test_comm_init_deadline_when_a_rank_never_joins():
     while _threads() > base and time.monotonic() < deadline:
         time.sleep(0.1)
     assert _threads() <= base, (_threads(), base)
+
+
+def test_comm_init_with_the_system_rccl():
+    """The Go host loads /opt/rocm's RCCL (libnas.so's own dependency), the
+    Python tests torch's copy, which this process already mapped: run the
+    one-rank communicator + a pass in a child that never imports torch."""
+    import subprocess
+    import sys
+    code = ("import sys; from kubernetesnetawarescheduler_amd import Engine\n"
+            "with Engine(0) as e:\n"
+            "    e.comm_init(Engine.comm_unique_id(), 0, 1)\n"
+            "    e.synth_cluster(7, 512, 2048, 'i8', peers=8)\n"
+            "    n, _, _ = e.place()\n"
+            "    assert (n >= -1).all()\n"
+            "assert 'torch' not in sys.modules\n"
+            "print('rccl', [l.split()[-1] for l in open('/proc/self/maps') if 'librccl' in l][:1])\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "/opt/rocm" in r.stdout, r.stdout
