@@ -112,6 +112,10 @@ constexpr bool cost_wide() {
     return DT == NAS_DT_I8 ? COST_WIDE_I8 : COST_WIDE_BF16;
 }
 
+#ifndef COST_OVF_EARLY
+#define COST_OVF_EARLY 0
+#endif
+
 template <int DT>
 struct Mma;
 
@@ -218,6 +222,11 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     using M = Mma<DT>;
     using acc_t = typename M::acc_t;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    // the fused fit's words after the main loop: behind the cross-wave merge's
+    // lists ([NWN][NI][32][9] u64), inside the smallest staging image
+    constexpr int FIT_LDS_OFF = 32768;
+    static_assert(FIT_LDS_OFF >= NWN * NI * 32 * 9 * 8 &&
+                  FIT_LDS_OFF + NW * NI * 2 * 64 * 8 <= 2 * STG, "fused-fit LDS words");
 
     // ---- XCD-aware tile order: blocks b, b+8, ... share an XCD (speed only)
     const int nwg = n_mt * n_nt;
@@ -267,7 +276,13 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // launch's, or the WA_PAD_ROWS padding) and are never written
     const int p_end = (BNK != BN && !dyn_start) ? dyn_hi : 0x7fffffff;
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // (the wide tile: the wave index wave-uniform in SGPRs, and the lane index
+    // re-derived after the main loop -- see below -- so that nothing per-lane
+    // outlives the loop beside the 128 accumulators: at three waves per SIMD
+    // the loop fills the 168 registers, and values held across it spilled)
+    const int tid = threadIdx.x;
+    int lane = tid & 63;
+    const int w = NWN == 6 ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     const int wm = w / NWN, wn = w % NWN;
 
     const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
@@ -376,9 +391,15 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                                             : -1;
         }
     };
-    // fit words: bit j of mw[ni][mi2] = the lane's pod of group ni fits node
-    // wm*128 + mi2*64 + j of the tile
-    auto fit_words = [&](u64 (&mw)[NI][2]) {
+    // fit words: bit j of word (ni, mi2) = the lane's pod of group ni fits
+    // node wm*128 + mi2*64 + j of the tile; each lane stores its own words in
+    // LDS (fit_slot, past the cross-wave merge's region) and reads them back
+    // per pod group in the epilogue (held in registers beside the 128
+    // accumulators they spilled: 24 B of scratch per lane)
+    auto fit_slot = [&](int ni, int mi2) -> u64 * {
+        return reinterpret_cast<u64 *>(lds + FIT_LDS_OFF) + ((w * NI + ni) * 2 + mi2) * 64 + lane;
+    };
+    auto fit_words = [&]() {
 #pragma unroll
         for (int mi2 = 0; mi2 < 2; ++mi2) {
             const bool real = mt * BM + wm * 128 + mi2 * 64 + lane < fs.nloc;
@@ -413,7 +434,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                                   __builtin_amdgcn_ballot_w64(rd <= fcap[mi2][2]);
                     if ((lane & 31) == i) word = m;
                 }
-                mw[ni][mi2] = word;
+                *fit_slot(ni, mi2) = word;
             }
         }
     };
@@ -436,12 +457,18 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = acc_t{};
-    const int fr = lane & 31, fh = lane >> 5;
+    int fr = lane & 31, fh = lane >> 5;
     // ---- exact int32 traffic: the entries outside the int8 plane (nas::Ovf):
     // e * L[m][n] for the lane's 64 nodes per pod are the accumulators'
     // initial value (4 dwords of Lr per 32-node tile: rows (reg & 3) +
-    // 8 * (reg >> 2) + 4 * fh are 4 groups of 4 consecutive nodes)
-    if constexpr (DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
+    // 8 * (reg >> 2) + 4 * fh are 4 groups of 4 consecutive nodes).  Both pod
+    // groups' list bounds load together, and an entry's 16 row dwords (all
+    // four 32-node tiles) in one round, so an entry costs two dependent
+    // loads, not eight; the two-stage pipeline runs this behind its first
+    // stage's LDS-DMA (the prologue waits once for both)
+    if constexpr (NWN == 6 && DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
+        // (the wide tile: inline, in the layout of rounds 1-2 -- its registers
+        // allow one tile's row dwords at a time)
         if (ov.ptr) {
             const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
             const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
@@ -470,6 +497,50 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             }
         }
     }
+    constexpr bool OVF_EARLY = COST_OVF_EARLY;
+    auto seed_ovf = [&]() __attribute__((always_inline)) {
+        if constexpr (NWN != 6 && DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
+            if (ov.ptr) {
+                const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
+                const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
+                // pod group ni's entries [beg, end)
+                auto bounds = [&](int ni, int &beg, int &end) {
+                    const int r = p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31);
+                    beg = end = 0;
+                    if (r < cnt_lim && r < p_end) {
+                        const int pod = (ov.row_pod ? ov.row_pod[r] : r) + cb * Pp;
+                        beg = ov.ptr[pod];
+                        end = ov.ptr[pod + 1];
+                    }
+                };
+                {
+                    int beg[NI], end[NI];
+#pragma unroll
+                    for (int ni = 0; ni < NI; ++ni) bounds(ni, beg[ni], end[ni]);
+#pragma unroll
+                    for (int ni = 0; ni < NI; ++ni)
+                        for (int j = beg[ni]; j < end[ni]; ++j) {
+                            const int e = ov.e[j];
+                            const signed char *row = lr + (size_t)ov.m[j] * (n_mt * BM);
+                            int v[4][4];
+#pragma unroll
+                            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                                for (int g = 0; g < 4; ++g)
+                                    v[mi][g] = *reinterpret_cast<const int *>(row + mi * 32 + 8 * g);
+#pragma unroll
+                            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                                    for (int c = 0; c < 4; ++c)
+                                        acc[mi][ni][4 * g + c] += e * (int)(signed char)(v[mi][g] >> (8 * c));
+                        }
+                }
+            }
+        }
+    };
+    if constexpr (PIPE != 0 || OVF_EARLY) seed_ovf();
 
     // fragments of k-substep kk+1 are read from LDS while the 8 MFMAs of kk
     // run (register double buffer; the just-in-time schedule hipcc picks on
@@ -730,6 +801,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         // two-stage pipeline: stage t+1 streams in (LDS-DMA) while t is read
         stageA(0, 0);
         stageB(0, 0);
+        if constexpr (!OVF_EARLY) seed_ovf();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         for (int t = 0; t < nk; ++t) {
@@ -789,13 +861,22 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             }
         return;
     }
+    if constexpr (NWN == 6) {
+        // the lane index afresh (volatile: not CSE'd with the prologue's), so
+        // the old one dies in the loop
+        int l;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+        lane = l;
+        fr = l & 31;
+        fh = l >> 5;
+    }
     if constexpr (FUSE) {
         // the fused fit, after the main loop: nothing of it is live across
         // the loop (held there, its registers pushed the loop's LDS-DMA
         // addresses into scratch: the launch ran 12-24% slower); the loads'
         // latency (~1 us of L2) is exposed once per workgroup
         fit_issue();
-        fit_words(mwp);
+        fit_words();
     }
     // ---- epilogue: fit mask + per-pod candidate list
     // per lane: top-4 of its 64 (node, cost) values per pod; lanes l and l^32
@@ -804,7 +885,12 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     u64 key[NI][8], bnd[NI];
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
-        const u64 *mw = mwp[ni];
+        u64 mwf[2];
+        if constexpr (FUSE) {
+#pragma unroll
+            for (int mi2 = 0; mi2 < 2; ++mi2) mwf[mi2] = *fit_slot(ni, mi2);
+        }
+        const u64 *mw = FUSE ? mwf : mwp[ni];
         // orderable keys of the lane's 64 (node, cost) values and their range
         // (int8: the range of the raw int32 costs -- the key is x ^ 2^31, so
         // key differences are cost differences)

@@ -836,9 +836,18 @@ constexpr int CHUNK_WORKGROUPS = 512;  // cost workgroups per big chunk (measure
                              // workgroups at 40 node tiles, as the 256-pod form's 32-unit chunks);
                              // 24 / 33 units measured 0.5-2% slower (profiles/r02_s4_ab_chunk.txt)
 #endif
+// node tiles per rank for chunk planning: the LARGEST shard's, the same on
+// every rank (rank shards differ by up to one node, so their own Mp can
+// differ by a tile, e.g. 2,049 nodes over 8 ranks: 256 vs 257 nodes); every
+// rank must plan the same chunks, or their per-chunk all-gathers mismatch
+int plan_n_mt(const nas_ctx *ctx) {
+    const int64_t widest = ((int64_t)ctx->N + ctx->world - 1) / ctx->world;
+    return (int)(nas::round_up(std::max<int64_t>(widest, 1), nas::COST_BM) / nas::COST_BM);
+}
+
 int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     const int wgs = CHUNK_WORKGROUPS;
-    const int n_mt = ctx->Mp / nas::COST_BM;
+    const int n_mt = plan_n_mt(ctx);
     const int big = std::max(32, (wgs + n_mt - 1) / n_mt);
     // 32-tile chunks (whole waves of workgroups at 8+ node tiles) with a
     // short last one; when the workgroup target sets the size (a node shard
@@ -877,6 +886,83 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     const int unit = tile_pods(ctx) / std::gcd(tile_pods(ctx), nas::COST_BN);
     tiles = std::min(left, (tiles + unit - 1) / unit * unit);
     return tiles * nas::COST_BN;
+}
+
+#ifndef CHUNK_BALANCE
+#define CHUNK_BALANCE 1
+#endif
+#ifndef CHUNK_BALANCE_SHARD
+#define CHUNK_BALANCE_SHARD 1
+#endif
+// The pass's scoring chunks [lo, hi) in pod order; chunk c runs on scoring
+// stream c & 1.  On the wide tile (one cluster, G = 1) the two streams'
+// totals are balanced at the end: the remainder after the 48-unit chunks is
+// split over one last chunk per stream, sized so that both streams carry the
+// same number of units and finish together (with the last chunks alternating
+// as before, the stream that drew the first full chunk carried ~37 more wide
+// tiles of 261 at C3, and ran alone -- one partial wave of idle CUs per
+// chunk -- for the last ~1.4 ms of the scoring: profiles/r03_pass_timeline_c3_*.txt,
+// r03_ab_balance_ksweep.txt)
+std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
+    std::vector<std::pair<int, int>> chunks;
+    const int P = ctx->P;
+    const bool wide = tile_pods(ctx) != nas::COST_BN;
+    // a node shard with few node tiles: equal chunks of ~CHUNK_WORKGROUPS
+    // cost workgroups (chunk_pods mode 2), balanced the same way
+    const int n_mt = plan_n_mt(ctx);
+    const int big_ns = std::max(32, (CHUNK_WORKGROUPS + n_mt - 1) / n_mt);
+    const bool shard = !wide && big_ns > 32 && ctx->B == 1;
+    if (!((CHUNK_BALANCE && wide) || (CHUNK_BALANCE_SHARD && shard))) {
+        for (int c = 0, lo = 0; lo < P; ++c) {
+            const int hi = std::min(P, lo + chunk_pods(ctx, c, lo));
+            chunks.push_back({lo, hi});
+            lo = hi;
+        }
+        return chunks;
+    }
+    const int unit = tile_pods(ctx) / std::gcd(tile_pods(ctx), nas::COST_BN);  // wide: 3 (256-pod units)
+    const int total = (P + nas::COST_BN - 1) / nas::COST_BN;                   // 256-pod units
+    std::vector<int> sizes;
+    int load[2] = {0, 0}, left = total;
+    auto take = [&](int u) {
+        u = std::min(left, (u + unit - 1) / unit * unit);
+        sizes.push_back(u);
+        load[(sizes.size() - 1) & 1] += u;
+        left -= u;
+    };
+    // wide: 48-unit chunks, the second stream's first one half as long; node
+    // shard: a 32-tile first chunk (the commit stream starts early), then
+    // `big_ns`-tile chunks
+    const int big = wide ? CHUNK_TILES_WIDE : big_ns;
+    const int first = wide ? big : 32, second = wide ? big / 2 : big;
+    if (left <= big) {
+        take(left);
+    } else {
+        take(first);
+        take(second);
+        while (left > 0) {
+            // can the rest end as one chunk on the next stream s and one on
+            // the other, both at most `big`, with equal stream totals?
+            const int s = sizes.size() & 1;
+            const int x = std::max(0, (left + load[s ^ 1] - load[s]) / 2) / unit * unit;
+            if (x >= unit && x <= big && left - x <= big) {
+                take(x);
+                if (left > 0) take(left);
+                break;
+            }
+            if (x < unit && left <= big) {  // stream s is ahead: one last chunk
+                take(left);
+                break;
+            }
+            take(big);
+        }
+    }
+    for (int lo = 0, i = 0; i < (int)sizes.size(); ++i) {
+        const int hi = std::min(P, lo + sizes[i] * nas::COST_BN);
+        chunks.push_back({lo, hi});
+        lo = hi;
+    }
+    return chunks;
 }
 
 int alloc_extended(nas_ctx *ctx) {
@@ -1756,12 +1842,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // chunk bounds; every scoring launch is enqueued before any commit-stream
     // work, so the host's enqueue time of merges / commits / copies never
     // delays the next chunk's cost launch
-    std::vector<std::pair<int, int>> chunks;
-    for (int c = 0, lo = 0; lo < P; ++c) {
-        const int hi = std::min(P, lo + chunk_pods(ctx, c, lo));
-        chunks.push_back({lo, hi});
-        lo = hi;
-    }
+    const std::vector<std::pair<int, int>> chunks = plan_chunks(ctx);
     // a one-chunk pass without a communicator has nothing to pipeline: its
     // merge / commit / copies stay on the scoring stream, which saves the
     // cross-stream event hops (~15-20 us each) that dominate a small pass

@@ -9,13 +9,13 @@ import sys
 
 
 def main(d, la="A", lb="B"):
-    for f in sorted(glob.glob(os.path.join(d, "[AB]_*.json"))):
+    for f in sorted(glob.glob(os.path.join(d, "[A-F]_*.json"))):
         try:
             p = json.load(open(f))
         except (ValueError, OSError):
             print(os.path.basename(f), "unreadable")
             continue
-        tag = la if os.path.basename(f).startswith("A") else lb
+        tag = {"A": la, "B": lb}.get(os.path.basename(f)[0], os.path.basename(f)[0])
         rf = p.get("roofline", {})
         fr = p.get("fit_roofline", {})
         cf = p.get("configs", {})
