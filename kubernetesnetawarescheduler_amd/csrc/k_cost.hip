@@ -441,17 +441,21 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 
     // the epilogue's fit-mask words, loaded now so their latency hides
     // under the main loop (k_fit wrote them before this launch)
+    // (issued after the overflow seeding, whose loop they would otherwise
+    // stay live across)
     u64 mwp[NI][2];
-    if constexpr (!FUSE && (EPI == 0 || EPI == 2 || EPI == 6)) {
+    auto load_mask = [&]() __attribute__((always_inline)) {
+        if constexpr (!FUSE && (EPI == 0 || EPI == 2 || EPI == 6)) {
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni)
+            for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-            for (int mi2 = 0; mi2 < 2; ++mi2) {
-                const int pod = min(p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31), p_end - 1);
-                const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
-                mwp[ni][mi2] = mask[(size_t)chunk * Pp + pod];
-            }
-    }
+                for (int mi2 = 0; mi2 < 2; ++mi2) {
+                    const int pod = min(p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31), p_end - 1);
+                    const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
+                    mwp[ni][mi2] = mask[(size_t)chunk * Pp + pod];
+                }
+        }
+    };
     acc_t acc[4][NI];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -541,6 +545,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         }
     };
     if constexpr (PIPE != 0 || OVF_EARLY) seed_ovf();
+    if constexpr (PIPE != 0 || OVF_EARLY || NWN == 6) load_mask();
 
     // fragments of k-substep kk+1 are read from LDS while the 8 MFMAs of kk
     // run (register double buffer; the just-in-time schedule hipcc picks on
@@ -802,6 +807,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         stageA(0, 0);
         stageB(0, 0);
         if constexpr (!OVF_EARLY) seed_ovf();
+        if constexpr (!OVF_EARLY && NWN != 6) load_mask();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         for (int t = 0; t < nk; ++t) {
@@ -923,28 +929,52 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             // insert of x into c0 <= .. <= c3: c3 = med3(c2, c3, x), c2 =
             // med3(c1, c2, x), c1 = med3(c0, c1, x), c0 = min(c0, x).
             unsigned c0 = 0xffffffffu, c1 = c0, c2 = c0, c3 = c0;
-            // int8: raw = cost bits, base = min cost; bf16: raw = key, base = kmin
+            // int8 with every lane's costs in [0, 2^26 - 1) (the common case:
+            // non-negative traffic and latency): x = cost << 6 | i directly
+            // (key base = okey(0)); otherwise relative to the lane's base
+            // (int8: raw = cost bits, base = min cost; bf16: raw = key, base =
+            // kmin).  Epilogue VALU per value 8 -> 5 (direct, every node of the
+            // 32-node half fitting every lane's pod: one v_lshl_or_b32) / 7
+            // (PMC: the epilogue is VALU-issue-bound, 1,377 instructions per
+            // wave = ~10% of a C5 launch, profiles/r03_pmc_epilogue.txt)
+            const bool direct = DT == NAS_DT_I8 && __all(smin >= 0 && smax < (1 << 26) - 1);
+            const unsigned kbase = direct ? 0x80000000u : kmin;
             const unsigned nk6 = 0u - ((DT == NAS_DT_I8 ? (unsigned)smin : kmin) << 6);
+            auto insert = [&](unsigned x) {
+                c3 = umed3(c2, c3, x);
+                c2 = umed3(c1, c2, x);
+                c1 = umed3(c0, c1, x);
+                c0 = min(c0, x);
+            };
 #pragma unroll
             for (int mi2 = 0; mi2 < 2; ++mi2)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int mi = mi2 * 2 + h;
-                    const unsigned nbits = ~(unsigned)(mw[mi2] >> (32 * h));
+                    const unsigned bitsw = (unsigned)(mw[mi2] >> (32 * h));
+                    const unsigned nbits = ~bitsw;
+                    if (direct && __all(bitsw == 0xffffffffu)) {
 #pragma unroll
-                    for (int reg = 0; reg < 16; ++reg) {
-                        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
-                        // (key << 6) - (kmin << 6) = (key - kmin) << 6 (v_lshl_add),
-                        // slot and the sign-extended not-fit bit (v_bfe_i32) OR'ed in
-                        const unsigned raw = DT == NAS_DT_I8 ? (unsigned)(int)acc[mi][ni][reg]
-                                                             : u[mi][reg];
-                        const unsigned x = ((raw << 6) + nk6) |
-                                           (unsigned)(mi * 16 + reg) |
-                                           (unsigned)__builtin_amdgcn_sbfe((int)nbits, row, 1);
-                        c3 = umed3(c2, c3, x);
-                        c2 = umed3(c1, c2, x);
-                        c1 = umed3(c0, c1, x);
-                        c0 = min(c0, x);
+                        for (int reg = 0; reg < 16; ++reg)
+                            insert(((unsigned)(int)acc[mi][ni][reg] << 6) | (unsigned)(mi * 16 + reg));
+                    } else {
+#pragma unroll
+                        for (int reg = 0; reg < 16; ++reg) {
+                            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
+                            const unsigned raw = DT == NAS_DT_I8 ? (unsigned)(int)acc[mi][ni][reg]
+                                                                 : u[mi][reg];
+                            // (raw << 6) - (base << 6) in one v_lshl_add (hipcc
+                            // otherwise emits a subtract and a shift); slot and
+                            // the sign-extended not-fit bit (v_bfe_i32) OR'ed in
+                            unsigned y;
+                            if (direct) {
+                                y = raw << 6;
+                            } else {
+                                asm("v_lshl_add_u32 %0, %1, 6, %2" : "=v"(y) : "v"(raw), "v"(nk6));
+                            }
+                            insert(y | (unsigned)(mi * 16 + reg) |
+                                   (unsigned)__builtin_amdgcn_sbfe((int)nbits, row, 1));
+                        }
                     }
                 }
             const unsigned cc[4] = {c0, c1, c2, c3};
@@ -954,7 +984,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                 const unsigned i = cc[j] & 63u, r = i & 15u;
                 const unsigned node = nb + (i >> 4) * 32u + (r & 3u) + 8u * (r >> 2);
                 k4[j] = cc[j] == 0xffffffffu ? KEY_INVALID
-                                             : ((u64)((cc[j] >> 6) + kmin) << 32) | node;
+                                             : ((u64)((cc[j] >> 6) + kbase) << 32) | node;
             }
         } else {
             Top4 t4;

@@ -418,7 +418,11 @@ int nccl_enqueued(nas_ctx *ctx, ncclComm *cm, ncclResult_t r, const char *what) 
                                  " ms (NAS_OPT_COMM_TIMEOUT_MS): communicators aborted, "
                                  "context poisoned");
         }
-        std::this_thread::sleep_for(std::chrono::microseconds(20));
+        // spin (yield) for the first ms: a sleep costs ~60-80 us of timer
+        // slack per poll, on the pass's critical path when the enqueue of a
+        // chunk's all-gather is what the commit stream waits for
+        if (clk::now() - t0 < std::chrono::milliseconds(1)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     if (r != ncclSuccess)
         return nas::fail(ctx, NAS_ERR_COMM, std::string(what) + ": " + ncclGetErrorString(r));
@@ -497,6 +501,9 @@ int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, ncc
     return NAS_OK;
 }
 
+#ifndef NAS_FUSE_SHARD
+#define NAS_FUSE_SHARD 0
+#endif
 // scoring for pods [p_lo, p_hi) on stream st against capacity `cap`:
 // fit -> cost/top-k, then (merge = true) merge_range on the same stream over
 // the stream's communicator
@@ -510,12 +517,22 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
     const int np = pr1 - pr0;
     auto *mask = ctx->mask.as<uint64_t>();
-    // the cost launch decides the fit itself (fused fit): no k_fit before it
+    // the cost launch decides the fit itself (fused fit): no k_fit before it.
+    // Not on a node shard (NAS_FUSE_SHARD 0): there the k_fit launch between
+    // two cost launches of a scoring stream is a gap in which the commit
+    // stream's merge / exchange / commit kernels get CUs; with back-to-back
+    // cost launches each of them waited ~100 us for a cost workgroup to
+    // drain (G = 8 rehearsal 1.53 vs 1.34 ms per pass in round 2:
+    // profiles/r03_g8_timeline_before.txt, r03_ab_fuse_shard.txt)
+    const bool fuse = NAS_FUSE_SHARD || ctx->world == 1;
     const nas::FitSrc fit{cap, v.req, ctx->N, ctx->Nloc0, ctx->Nloc};
     hipEvent_t e0 = tm.fine(st);
-    hipEvent_t e1 = e0;
+    if (!fuse)
+        HIPCK(nas::launch_fit(st, cap, ctx->N, ctx->Nloc0, ctx->Nloc, ctx->Mp, v.req, p_hi, v.Pp,
+                              p_lo, p_hi - p_lo, mask));
+    hipEvent_t e1 = fuse ? e0 : tm.fine(st);
     const nas::Ovf ov = make_ovf(ctx);
-    HIPCK(launch_cost(ctx, st, v.Pp, pr0, np, mask, nullptr, 1, &ov, nullptr, &fit));
+    HIPCK(launch_cost(ctx, st, v.Pp, pr0, np, mask, nullptr, 1, &ov, nullptr, fuse ? &fit : nullptr));
     hipEvent_t e2 = tm.fine(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
@@ -1859,10 +1876,14 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // above (overflow lists, latency rows, fp32 splits) are read by every
     // chunk's cost launch.
     if (!live_cap) OK(pass_init(st));
+    // the two scoring streams (a CU-masked pair that left 8 or 16 CUs to the
+    // commit stream on node shards measured 25-35% slower at G = 8:
+    // profiles/r03_ab_reserve_cus.txt)
+    const hipStream_t ss2[2] = {st, ctx->stream2};
     if (!one_stream) {
         hipEvent_t ready = tm.mark(st);
-        HIPCK(hipStreamWaitEvent(ctx->stream2, ready, 0));
-        HIPCK(hipStreamWaitEvent(sc, ready, 0));
+        for (hipStream_t s : {ss2[0], ss2[1], sc})
+            if (s != st) HIPCK(hipStreamWaitEvent(s, ready, 0));
     }
     std::vector<hipEvent_t> scored(chunks.size());
     // fit + cost only on the two scoring streams (a chunk's tail blocks overlap
@@ -1871,7 +1892,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // communicator) each chunk right before committing it, so no cost launch
     // ever waits behind a merge or an all-gather
     for (size_t c = 0; c < chunks.size(); ++c) {
-        hipStream_t ss = (c & 1) ? ctx->stream2 : st;
+        hipStream_t ss = ss2[c & 1];
         OK(score_range(ctx, tm, chunks[c].first, chunks[c].second, ss, score_cap, nullptr, false));
         scored[c] = tm.mark(ss);
     }
@@ -1886,7 +1907,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         const bool tail = !one_stream && c + 1 == chunks.size();
         hipStream_t cs = sc;
         if (tail) {
-            cs = (c & 1) ? ctx->stream2 : st;
+            cs = ss2[c & 1];
             HIPCK(hipStreamWaitEvent(cs, tm.mark(sc), 0));
         } else {
             HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
@@ -1909,9 +1930,9 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     }
     // st must follow everything: the last chunk's stream followed the commit
     // stream, which followed every earlier chunk's scoring; so st waits only
-    // when the last chunk ran on stream2
-    if (!one_stream && chunks.size() % 2 == 0)
-        HIPCK(hipStreamWaitEvent(st, tm.mark(ctx->stream2), 0));
+    // when the last chunk ran on another stream
+    if (!one_stream && ss2[(chunks.size() - 1) & 1] != st)
+        HIPCK(hipStreamWaitEvent(st, tm.mark(ss2[(chunks.size() - 1) & 1]), 0));
     if (ctx->comm) inject_stall(ctx, st);  // behind every collective of the pass
     // speculative slots: as many as the previous pass of this shape needed
     // (consecutive passes over similar clusters stop alike), enqueued before
@@ -2176,6 +2197,9 @@ int nas_comm_unique_id(uint8_t id_out[128]) {
     return NAS_OK;
 }
 
+#ifndef NAS_COMM_CHILD_BLOCKING
+#define NAS_COMM_CHILD_BLOCKING 0
+#endif
 int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world) {
     NAS_RANGE("nas_comm_init");
     OK(bind(ctx));
@@ -2304,7 +2328,7 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
         for (int i = 0; i < 3 && r == ncclSuccess; ++i) {
             what = "ncclCommInitRankConfig (child)";
             ncclConfig_t kc = NCCL_CONFIG_INITIALIZER;
-            kc.blocking = 0;
+            kc.blocking = NAS_COMM_CHILD_BLOCKING;
             r = ncclCommInitRankConfig(&st->kids[i], world, kid_ids[i], rank, &kc);
             if (r == ncclInProgress && load(&st->kids[i])) r = settle(load(&st->kids[i]));
             if (r == ncclSuccess && !load(&st->kids[i])) r = ncclInternalError;

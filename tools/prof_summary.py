@@ -40,7 +40,8 @@ def per_dispatch(d):
     """{(dispatch id, short kernel, grid): {counter: summed value}}"""
     per = {}
     for r in rows(os.path.join(d, "**", "*counter_collection.csv")):
-        key = (int(r["Dispatch_Id"]), short(r["Kernel_Name"]), int(r.get("Grid_Size", 0) or 0))
+        key = (int(r["Dispatch_Id"]), short(r["Kernel_Name"]), int(r.get("Grid_Size", 0) or 0),
+               r["Kernel_Name"])
         c = per.setdefault(key, {})
         c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return per
@@ -60,11 +61,13 @@ def main(d):
     # mean kernel durations of the headline grid in the bench trace (for the clock)
     dur = {}
     for r in rows(f"{d}/trace_bench/**/*kernel_trace.csv"):
-        k = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]))
+        # (full name: the int8 and bf16 instantiations share a grid at C3)
+        k = (r["Kernel_Name"],
+             int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r.get("Grid_Size_Z", 1) or 1))
         dur.setdefault(k, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     merged = {}
     for sub in ("pmc1", "pmc2", "pmc3"):
-        for (disp, kern, grid), c in per_dispatch(os.path.join(d, sub)).items():
+        for (disp, kern, grid, full), c in per_dispatch(os.path.join(d, sub)).items():
             if kern not in ("k_cost_topk", "k_fit", "k_merge"):
                 continue
             # the largest dispatch per kernel: by the counter that scales with work
@@ -73,6 +76,8 @@ def main(d):
             if score >= m.get(sub + "_score", -1):
                 m[sub + "_score"] = score
                 m[sub] = c
+                if sub == "pmc1":
+                    m["grid"] = (full, grid)
     for kern, m in merged.items():
         out = {}
         sq = m.get("pmc1", {})
@@ -86,9 +91,10 @@ def main(d):
             out["GRBM_GUI_ACTIVE_per_xcd"] = gui
             out["mfma_busy_frac"] = sq.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (gui * 1024)
             out["SQ_INSTS_LDS"] = sq.get("SQ_INSTS_LDS")
-            cands = [v for (k, _), v in dur.items() if k == kern]
-            if cands:  # the largest grid of that kernel in the bench trace
-                big = max(dur.items(), key=lambda kv: (kv[0][0] == kern, kv[0][1]))[1]
+            # the bench trace's dispatches of the same kernel at the same grid
+            # as the profiled one (the largest grid overall is C4's or C5's)
+            big = dur.get(m.get("grid", ("", -1)))
+            if big:
                 mean_s = sum(big) / len(big)
                 # GRBM_GUI_ACTIVE counts the whole counter window of the
                 # dispatch (set-up and drain included), so for a short kernel
