@@ -470,9 +470,15 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // four 32-node tiles) in one round, so an entry costs two dependent
     // loads, not eight; the two-stage pipeline runs this behind its first
     // stage's LDS-DMA (the prologue waits once for both)
-    if constexpr (NWN == 6 && DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
-        // (the wide tile: inline, in the layout of rounds 1-2 -- its registers
-        // allow one tile's row dwords at a time)
+    // (the layout of rounds 1-2, inline: the wide tile, whose registers allow
+    // one tile's row dwords at a time, and the 256 x 256 launches without the
+    // fused fit -- node shards, rescore windows -- which must stay at <= 192
+    // VGPRs: a node shard's merge / all-gather / commit kernels run beside a
+    // cost workgroup only while its two waves per SIMD leave registers free
+    // (at 256 VGPRs the G = 8 rehearsal pass rose from 1.39 to 1.50 ms:
+    // profiles/r03_bisect_g8.txt))
+    constexpr bool OVF_ROUND2 = NWN == 6 || !FUSE;
+    if constexpr (OVF_ROUND2 && DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
         if (ov.ptr) {
             const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
             const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
@@ -503,7 +509,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     }
     constexpr bool OVF_EARLY = COST_OVF_EARLY;
     auto seed_ovf = [&]() __attribute__((always_inline)) {
-        if constexpr (NWN != 6 && DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
+        if constexpr (!OVF_ROUND2 && DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
             if (ov.ptr) {
                 const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
                 const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;

@@ -908,6 +908,9 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
 #ifndef CHUNK_BALANCE
 #define CHUNK_BALANCE 1
 #endif
+#ifndef SCORE_STREAMS
+#define SCORE_STREAMS 2
+#endif
 #ifndef CHUNK_BALANCE_SHARD
 #define CHUNK_BALANCE_SHARD 1
 #endif
@@ -1879,7 +1882,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // the two scoring streams (a CU-masked pair that left 8 or 16 CUs to the
     // commit stream on node shards measured 25-35% slower at G = 8:
     // profiles/r03_ab_reserve_cus.txt)
-    const hipStream_t ss2[2] = {st, ctx->stream2};
+    const hipStream_t ss2[2] = {st, SCORE_STREAMS == 1 && ctx->world == 1 ? st : ctx->stream2};
     if (!one_stream) {
         hipEvent_t ready = tm.mark(st);
         for (hipStream_t s : {ss2[0], ss2[1], sc})
