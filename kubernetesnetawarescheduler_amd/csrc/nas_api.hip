@@ -911,8 +911,11 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
 #ifndef SCORE_STREAMS
 #define SCORE_STREAMS 2
 #endif
+// Node shards keep equal chunks: the balanced plan below put two chunk chains
+// in the pass's tail and measured 4-8% slower at G = 8 and 1% at G = 4
+// (profiles/r03_ab_chunk_plan_shard.txt)
 #ifndef CHUNK_BALANCE_SHARD
-#define CHUNK_BALANCE_SHARD 1
+#define CHUNK_BALANCE_SHARD 0
 #endif
 // The pass's scoring chunks [lo, hi) in pod order; chunk c runs on scoring
 // stream c & 1.  On the wide tile (one cluster, G = 1) the two streams'
@@ -928,7 +931,8 @@ std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
     const int P = ctx->P;
     const bool wide = tile_pods(ctx) != nas::COST_BN;
     // a node shard with few node tiles: equal chunks of ~CHUNK_WORKGROUPS
-    // cost workgroups (chunk_pods mode 2), balanced the same way
+    // cost workgroups (chunk_pods mode 2); balanced the same way only when
+    // built with CHUNK_BALANCE_SHARD=1
     const int n_mt = plan_n_mt(ctx);
     const int big_ns = std::max(32, (CHUNK_WORKGROUPS + n_mt - 1) / n_mt);
     const bool shard = !wide && big_ns > 32 && ctx->B == 1;
