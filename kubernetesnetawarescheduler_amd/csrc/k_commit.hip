@@ -218,12 +218,29 @@ __device__ __forceinline__ void cap_to_lds(const int *g, int *l, int n3, int wav
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// The launch's placements [p_begin, p_end) (and their raw keys) into the
+// host's pinned stage, for the host to unpack while later chunks still run:
+// a launch of its own per array behind every commit (copy kernels) waited
+// 100-170 us each for a CU beside the wide cost workgroups and put four more
+// dependent launches into the pass's tail.  Pods past a halt carry stale
+// values here exactly as the copies did; the host re-reads everything then.
+__device__ __forceinline__ void to_stage(const int *out_node, const unsigned *out_cost,
+                                         int *stage_node, unsigned *stage_cost, int p_begin,
+                                         int p_end, int t, int nt) {
+    if (!stage_node) return;
+    for (int i = p_begin + t; i < p_end; i += nt) {
+        stage_node[i] = out_node[i];
+        if (stage_cost) stage_cost[i] = out_cost[i];
+    }
+}
+
 template <bool LDS_CAP>
 __global__ void __launch_bounds__(THREADS)
 k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
          const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
          int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
-         int *__restrict__ halt, int *__restrict__ pub, const unsigned char *__restrict__ zrow) {
+         int *__restrict__ halt, int *__restrict__ pub, const unsigned char *__restrict__ zrow,
+         int *__restrict__ stage_node, unsigned *__restrict__ stage_cost) {
     // one workgroup per cluster of a batched launch
     const int cb = blockIdx.x;
     cand_key += (size_t)cb * Pp * KC;
@@ -402,6 +419,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         halt[2] += round;  // rounds walked, reported in nas_timings
     }
     __syncthreads();
+    to_stage(out_node, out_cost, stage_node, stage_cost, p_begin, p_end, tid, THREADS);
     if (LDS_CAP)
         for (int i = tid; i < 3 * N; i += THREADS) cap_g[i] = capl[i];
 }
@@ -465,7 +483,8 @@ __global__ void __launch_bounds__(64)
 k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
            const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
            int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
-           int *__restrict__ halt, int *__restrict__ pub, const unsigned char *__restrict__ zrow) {
+           int *__restrict__ halt, int *__restrict__ pub, const unsigned char *__restrict__ zrow,
+           int *__restrict__ stage_node, unsigned *__restrict__ stage_cost) {
     const int cb = blockIdx.x;
     cand_key += (size_t)cb * Pp * KC;
     cand_bound += (size_t)cb * Pp;
@@ -677,6 +696,8 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         if (stop < p_end) *halt = stop;
         halt[2] += round;
     }
+    __syncthreads();  // (one wave: every lane's placements written)
+    to_stage(out_node, out_cost, stage_node, stage_cost, p_begin, p_end, lane, 64);
     if (LDS_CAP)
         for (int i = lane; i < 3 * N; i += 64) cap_g[i] = capl[i];
 }
@@ -688,8 +709,11 @@ bool commit_in_lds(int N) { return N <= LDS_CAP_MAX_NODES; }
 hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_t *cand_bound,
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost, int32_t *halt, int batch,
-                         int32_t *pub, const uint8_t *zrow) {
+                         int32_t *pub, const uint8_t *zrow, int32_t *stage_node,
+                         int32_t *stage_cost) {
     if (p_begin >= 0 && p_end <= p_begin) return hipSuccess;
+    if (stage_node && (p_begin < 0 || batch != 1)) return hipErrorInvalidValue;
+    auto *sc = reinterpret_cast<unsigned *>(stage_cost);
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
@@ -701,10 +725,10 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
                                         LDS_DYN_MAX, attr);
             if (e != hipSuccess) return e;
             k_commit_w<true><<<batch, 64, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
-                                                     out_node, oc, halt, nullptr, zrow);
+                                                     out_node, oc, halt, nullptr, zrow, stage_node, sc);
         } else {
             k_commit_w<false><<<batch, 64, PF_BYTES, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
-                                                           out_node, oc, halt, pub, zrow);
+                                                           out_node, oc, halt, pub, zrow, stage_node, sc);
         }
         return hipGetLastError();
     }
@@ -714,10 +738,10 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
         hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit<true>), LDS_DYN_MAX, attr);
         if (e != hipSuccess) return e;
         k_commit<true><<<batch, THREADS, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
-                                                oc, halt, nullptr, zrow);
+                                                oc, halt, nullptr, zrow, stage_node, sc);
     } else {
         k_commit<false><<<batch, THREADS, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
-                                               oc, halt, pub, zrow);
+                                               oc, halt, pub, zrow, stage_node, sc);
     }
     return hipGetLastError();
 }

@@ -1924,15 +1924,10 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         HIPCK(nas::launch_commit(cs, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
-                                 1, pub, zrow_ptr(ctx)));
+                                 1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr));
         tm.span(T_COMMIT, c0, tm.fine(cs));
-        // this chunk's results go to the pinned stage right behind its
-        // commit, and the host unpacks them while later chunks still run
-        HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo, (size_t)(hi - lo) * 4,
-                             hipMemcpyDeviceToHost, cs));
-        if (want_raw)
-            HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
-                                 (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, cs));
+        // the commit wrote this chunk's results into the pinned stage as it
+        // ended, and the host unpacks them while later chunks still run
         landed.push_back({lo, hi, tm.mark(cs)});
     }
     // st must follow everything: the last chunk's stream followed the commit
