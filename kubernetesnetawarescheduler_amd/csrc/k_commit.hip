@@ -224,10 +224,30 @@ __device__ __forceinline__ void cap_to_lds(const int *g, int *l, int n3, int wav
 // 100-170 us each for a CU beside the wide cost workgroups and put four more
 // dependent launches into the pass's tail.  Pods past a halt carry stale
 // values here exactly as the copies did; the host re-reads everything then.
+#ifndef STAGE_VEC
+#define STAGE_VEC 1
+#endif
 __device__ __forceinline__ void to_stage(const int *out_node, const unsigned *out_cost,
                                          int *stage_node, unsigned *stage_cost, int p_begin,
                                          int p_end, int t, int nt) {
     if (!stage_node) return;
+#if STAGE_VEC
+    // 16-byte stores while both stage arrays are aligned: a quarter of the
+    // store instructions over the host link
+    auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+    if (al(stage_node + p_begin) && al(out_node + p_begin) &&
+        (!stage_cost || (al(stage_cost + p_begin) && al(out_cost + p_begin)))) {
+        const int nv = (p_end - p_begin) >> 2;
+        for (int v = t; v < nv; v += nt) {
+            const int i = p_begin + 4 * v;
+            *reinterpret_cast<int4 *>(stage_node + i) = *reinterpret_cast<const int4 *>(out_node + i);
+            if (stage_cost)
+                *reinterpret_cast<uint4 *>(stage_cost + i) =
+                    *reinterpret_cast<const uint4 *>(out_cost + i);
+        }
+        p_begin += 4 * nv;
+    }
+#endif
     for (int i = p_begin + t; i < p_end; i += nt) {
         stage_node[i] = out_node[i];
         if (stage_cost) stage_cost[i] = out_cost[i];

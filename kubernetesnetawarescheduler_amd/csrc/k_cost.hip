@@ -1074,8 +1074,16 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 // does the bound: every intermediate kept[7] is >= the final kept[7], so the
 // result is min(all list bounds, final kept[7]) -- identical to a serial fold.
 constexpr int MERGE_LANES = 8;
+// 64 pods per workgroup (2 waves per SIMD at 56 VGPRs): still co-resides
+// with a 256 x 256 cost workgroup (2 waves per SIMD at 192 VGPRs) on a node
+// shard; 1,024-thread blocks do not, and measured 7% slower at G = 8 (the
+// wide tile admits nothing beside it either way: C3 within noise for 256 /
+// 512 / 1,024, profiles/r03_ab_merge_block.txt)
+#ifndef MERGE_BLOCK
+#define MERGE_BLOCK 512
+#endif
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(MERGE_BLOCK)
 k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_lists,
         long long stride, long long bstride, int src_p0, int p0, int np,
         u64 *__restrict__ dst, u64 *__restrict__ dst_bound, int dst_p0,
@@ -1233,7 +1241,8 @@ hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bo
     if (dyn) np = dyn->win;
     if (np <= 0) return hipSuccess;
     if (dst_idx && batch != 1) return hipErrorInvalidValue;
-    k_merge<<<dim3((int)(((int64_t)np * MERGE_LANES + 255) / 256), batch), 256, 0, st>>>(
+    k_merge<<<dim3((int)(((int64_t)np * MERGE_LANES + MERGE_BLOCK - 1) / MERGE_BLOCK), batch),
+              MERGE_BLOCK, 0, st>>>(
         reinterpret_cast<const u64 *>(keys), reinterpret_cast<const u64 *>(bounds), n_lists, stride,
         bstride, src_p0, p0, np, reinterpret_cast<u64 *>(cand_key),
         reinterpret_cast<u64 *>(cand_bound), dst_p0, dyn ? dyn->start : nullptr, dyn ? dyn->hi : 0,
