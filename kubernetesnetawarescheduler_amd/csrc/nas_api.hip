@@ -917,6 +917,12 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
 #ifndef CHUNK_BALANCE_SHARD
 #define CHUNK_BALANCE_SHARD 0
 #endif
+#ifndef CHUNK_FIRST_HALF
+#define CHUNK_FIRST_HALF 0
+#endif
+#ifndef CHUNK_MIN_TAIL
+#define CHUNK_MIN_TAIL 0  // 256-pod units: a stream's last chunk at least this long
+#endif
 // The pass's scoring chunks [lo, hi) in pod order; chunk c runs on scoring
 // stream c & 1.  On the wide tile (one cluster, G = 1) the two streams'
 // totals are balanced at the end: the remainder after the 48-unit chunks is
@@ -958,7 +964,12 @@ std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
     // shard: a 32-tile first chunk (the commit stream starts early), then
     // `big_ns`-tile chunks
     const int big = wide ? CHUNK_TILES_WIDE : big_ns;
-    const int first = wide ? big : 32, second = wide ? big / 2 : big;
+    // (CHUNK_FIRST_HALF=1 puts the half-length chunk first: chunks then finish
+    // in pod order and the in-order commit chain follows each chunk as it
+    // lands -- one merge + commit chain behind the scoring instead of four --
+    // but the pass measured the same or 0.5% slower: r03_ab_chunk_order.txt)
+    const int first = wide ? (CHUNK_FIRST_HALF ? big / 2 : big) : 32;
+    const int second = wide ? (CHUNK_FIRST_HALF ? big : big / 2) : big;
     if (left <= big) {
         take(left);
     } else {
@@ -980,6 +991,19 @@ std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
             }
             take(big);
         }
+    }
+    // (CHUNK_MIN_TAIL > 0: a stream's last chunk shorter than that takes
+    // units from the same stream's previous chunk -- stream totals and pod
+    // order stay.  C3's plan ends in a 3-unit chunk = 80 wide workgroups that
+    // runs nearly alone for one workgroup time, ~190 us,
+    // r03_pass_timeline_c3_final.txt, yet 12 / 18 measured within noise of
+    // it: r03_ab_chunk_order.txt.)
+    for (int i = std::max(2, (int)sizes.size() - 2); i < (int)sizes.size(); ++i) {
+        if (CHUNK_MIN_TAIL <= 0 || sizes[i] >= CHUNK_MIN_TAIL) continue;
+        const int d = (CHUNK_MIN_TAIL - sizes[i] + unit - 1) / unit * unit;
+        if (sizes[i - 2] - d < CHUNK_MIN_TAIL) continue;
+        sizes[i - 2] -= d;
+        sizes[i] += d;
     }
     for (int lo = 0, i = 0; i < (int)sizes.size(); ++i) {
         const int hi = std::min(P, lo + sizes[i] * nas::COST_BN);
