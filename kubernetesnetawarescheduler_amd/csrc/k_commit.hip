@@ -439,7 +439,8 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         halt[2] += round;  // rounds walked, reported in nas_timings
     }
     __syncthreads();
-    to_stage(out_node, out_cost, stage_node, stage_cost, p_begin, p_end, tid, THREADS);
+    to_stage(out_node, out_cost, stage_node ? stage_node + (size_t)cb * p_end : nullptr,
+             stage_cost ? stage_cost + (size_t)cb * p_end : nullptr, p_begin, p_end, tid, THREADS);
     if (LDS_CAP)
         for (int i = tid; i < 3 * N; i += THREADS) cap_g[i] = capl[i];
 }
@@ -717,7 +718,8 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         halt[2] += round;
     }
     __syncthreads();  // (one wave: every lane's placements written)
-    to_stage(out_node, out_cost, stage_node, stage_cost, p_begin, p_end, lane, 64);
+    to_stage(out_node, out_cost, stage_node ? stage_node + (size_t)cb * p_end : nullptr,
+             stage_cost ? stage_cost + (size_t)cb * p_end : nullptr, p_begin, p_end, lane, 64);
     if (LDS_CAP)
         for (int i = lane; i < 3 * N; i += 64) cap_g[i] = capl[i];
 }
@@ -732,7 +734,8 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
                          int32_t *pub, const uint8_t *zrow, int32_t *stage_node,
                          int32_t *stage_cost) {
     if (p_begin >= 0 && p_end <= p_begin) return hipSuccess;
-    if (stage_node && (p_begin < 0 || batch != 1)) return hipErrorInvalidValue;
+    // a batch stages whole clusters, [cluster][p_end] rows from pod 0
+    if (stage_node && (p_begin < 0 || (batch != 1 && p_begin != 0))) return hipErrorInvalidValue;
     auto *sc = reinterpret_cast<unsigned *>(stage_cost);
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);

@@ -697,17 +697,17 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
     HIPCK(hipMemcpyAsync(halt, hs, (size_t)B * nas::STATUS_INTS * 4, hipMemcpyHostToDevice, st));
     OK(score_batch(ctx, tm));
     hipEvent_t e3 = tm.mark(st);
-    HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
-                             ctx->req.as<int32_t>(), Pp, 0, P, ctx->cap.as<int32_t>(), N,
-                             ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt, B,
-                             nullptr, zrow_ptr(ctx)));
-    tm.span(T_COMMIT, e3, tm.mark(st));
-    // every cluster's placements (and raw scores) go to the pinned stage right
-    // behind the commit, before the status words: when no cluster stopped,
-    // the one status round trip brings the results with it
+    // every cluster's placements (and raw scores) go to the pinned stage from
+    // the commit kernel itself, before the status words: when no cluster
+    // stopped, the one status round trip brings the results with it
     int32_t *stage = reinterpret_cast<int32_t *>(ctx->host_status.as<char>() + host_out_offset(ctx->B));
     const size_t BP = (size_t)B * P;
     const bool want_raw = cost_out || int_score_out;
+    HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                             ctx->req.as<int32_t>(), Pp, 0, P, ctx->cap.as<int32_t>(), N,
+                             ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt, B,
+                             nullptr, zrow_ptr(ctx), stage, want_raw ? stage + BP : nullptr));
+    tm.span(T_COMMIT, e3, tm.mark(st));
     auto fetch = [&]() -> int {
         HIPCK(hipMemcpy2DAsync(stage, (size_t)P * 4, ctx->out_node.p, (size_t)Pp * 4,
                                (size_t)P * 4, B, hipMemcpyDeviceToHost, st));
@@ -716,7 +716,6 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
                                    (size_t)P * 4, B, hipMemcpyDeviceToHost, st));
         return NAS_OK;
     };
-    OK(fetch());
     hipEvent_t t1 = tm.mark(st);
     int slots = 0;
     while (true) {
