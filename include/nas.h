@@ -313,6 +313,22 @@ int nas_set_batch(nas_ctx *ctx, int32_t n_clusters);
 int nas_comm_unique_id(uint8_t id_out[128]);
 int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world);
 
+/* In-process transport instead of RCCL: `world` contexts of ONE process (on
+ * any devices, each driven by its own host thread) form a node-sharded
+ * placement whose exchanges are device-to-device pulls behind host barriers.
+ * Every call of nas_place / nas_score / nas_score_range / nas_score_reference
+ * then runs exactly the RCCL path's kernels, merges and commit with the
+ * all-gather replaced -- so G ranks' distinct candidate lists meet the
+ * cross-rank merge on one GPU (tests), or one host process drives the GPUs
+ * of a node without RCCL.  All ranks must make the same calls; a rank that
+ * does not arrive within NAS_OPT_COMM_TIMEOUT_MS breaks the group
+ * (NAS_ERR_COMM, contexts poisoned).  The group must outlive nas_comm_init_local;
+ * contexts keep it alive after nas_local_group_destroy. */
+typedef struct nas_local_group nas_local_group;
+int nas_local_group_create(int32_t world, nas_local_group **out);
+void nas_local_group_destroy(nas_local_group *group);
+int nas_comm_init_local(nas_ctx *ctx, nas_local_group *group, int32_t rank);
+
 /* Node shard without a communicator: this context keeps and scores only node
  * columns [rank*n/world, (rank+1)*n/world) (call before the extended
  * uploads).  For hosts that exchange candidate lists themselves (nas_score +

@@ -8,4 +8,4 @@ CustomScheduler lives in host/ (C++).
 """
 from ._lib import (K_CANDIDATES, NAS_DT_BF16, NAS_DT_I8, NAS_EMPTY, NAS_NONE, NasError,  # noqa: F401
                    LIB_PATH)
-from .engine import FIELDS, Engine  # noqa: F401
+from .engine import FIELDS, Engine, LocalGroup, local_ranks  # noqa: F401

@@ -96,6 +96,9 @@ SIGNATURES = {
     "nas_get_candidates": (_I, [_CTX, _V, _V, _V, _V, _V]),
     "nas_comm_unique_id": (_I, [_V]),
     "nas_comm_init": (_I, [_CTX, _V, _I, _I]),
+    "nas_local_group_create": (_I, [_I, _c.POINTER(_V)]),
+    "nas_local_group_destroy": (None, [_V]),
+    "nas_comm_init_local": (_I, [_CTX, _V, _I]),
     "nas_set_shard": (_I, [_CTX, _I, _I]),
     "nas_get_candidate_keys": (_I, [_CTX, _V, _V]),
     "nas_score_range": (_I, [_CTX, _I, _I]),

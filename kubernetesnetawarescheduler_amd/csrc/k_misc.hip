@@ -378,6 +378,19 @@ __global__ void k_rehearse_replicate(unsigned long long *__restrict__ a, long lo
     }
 }
 
+// In-process all-gather (nas_comm_init_local): dst[r][i] = src_r[i] for the
+// G ranks' send buffers, pulled by the receiving rank on its own stream.
+// blockIdx.y = source rank; 16-byte units when every pointer and the size
+// allow it, else 8-byte units (every exchanged record is a multiple of 8 B).
+template <typename U>
+__global__ void k_local_gather(LocalSrcs srcs, U *__restrict__ dst, long long n) {
+    const U *__restrict__ s = static_cast<const U *>(srcs.p[blockIdx.y]);
+    U *__restrict__ d = dst + (long long)blockIdx.y * n;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        d[i] = s[i];
+}
+
 // fp32 -> bf16, round to nearest even (finite inputs)
 __device__ __forceinline__ unsigned short bf16_rne(float x) {
     const unsigned u = __float_as_uint(x);
@@ -428,6 +441,22 @@ hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap,
 hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *buf, size_t n, int G, int N) {
     k_rehearse_replicate<<<grid_for((long long)n, 256), 256, 0, st>>>(
         reinterpret_cast<unsigned long long *>(buf), (long long)n, G, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_local_gather(hipStream_t st, const LocalSrcs &srcs, int G, void *dst,
+                               size_t bytes) {
+    if (G < 1 || G > LOCAL_MAX_WORLD || bytes % 8) return hipErrorInvalidValue;
+    if (bytes == 0) return hipSuccess;
+    bool v16 = bytes % 16 == 0 && reinterpret_cast<uintptr_t>(dst) % 16 == 0;
+    for (int r = 0; r < G; ++r) v16 = v16 && reinterpret_cast<uintptr_t>(srcs.p[r]) % 16 == 0;
+    const long long n = (long long)(bytes / (v16 ? 16 : 8));
+    const dim3 grid((unsigned)std::min<long long>((n + 255) / 256, 1024), G);
+    if (v16)
+        k_local_gather<uint4><<<grid, 256, 0, st>>>(srcs, static_cast<uint4 *>(dst), n);
+    else
+        k_local_gather<unsigned long long><<<grid, 256, 0, st>>>(
+            srcs, static_cast<unsigned long long *>(dst), n);
     return hipGetLastError();
 }
 

@@ -372,6 +372,9 @@ void split_row(const int64_t *v, int n, signed char *plane, std::vector<int32_t>
     }
 }
 
+// the call issued collectives other ranks must join (waits get deadlines)
+bool has_coll(const nas_ctx *ctx) { return ctx->comm != nullptr || ctx->local != nullptr; }
+
 int check_extended(nas_ctx *ctx) {
     if (!ctx->have_L || !ctx->have_cap || !ctx->have_pods || !ctx->have_wa)
         return nas::fail(ctx, NAS_ERR_STATE,
@@ -384,7 +387,7 @@ int check_extended(nas_ctx *ctx) {
         return nas::fail(ctx, NAS_ERR_ARG, "dtypes of latency / traffic differ");
     if (ctx->N != ctx->L_n || ctx->P != ctx->req_P || ctx->dtype != ctx->L_dtype)
         return nas::fail(ctx, NAS_ERR_STATE, "re-upload latency and traffic after resizing");
-    if (ctx->world > 1 && !ctx->comm && !ctx->virtual_shard)
+    if (ctx->world > 1 && !has_coll(ctx) && !ctx->virtual_shard)
         return nas::fail(ctx, NAS_ERR_STATE, "node shard without a communicator");
     // int8 path: exact int32 costs need sum_m |WA[p,m]| * |L[m,n]| <= INT32_MAX
     if (ctx->dtype == NAS_DT_I8 && ctx->wa_abs_row_max * (int64_t)ctx->L_abs_max > 0x7fffffffLL)
@@ -429,27 +432,205 @@ int nccl_enqueued(nas_ctx *ctx, ncclComm *cm, ncclResult_t r, const char *what) 
     return NAS_OK;
 }
 
-// all-gather each rank's per-pod lists (keys [np][KC] + bounds [np]) into
-// gk [world][np][KC] / gb [world][np] on `st` over communicator `cm`
-int exchange(nas_ctx *ctx, ncclComm *cm, hipStream_t st, const uint64_t *keys,
-             const uint64_t *bounds, size_t np, uint64_t *gk, uint64_t *gb) {
+// ---- collectives: RCCL (nas_comm_init) or the in-process transport
+// (nas_comm_init_local).  A channel is the stream family that issues them --
+// each keeps its own issue order on every rank: CH_SCORE (ctx->stream and
+// scoring stream 1), CH_SCORE2 (scoring stream 2), CH_COMMIT (the commit
+// stream and the pass's chunk merges).
+enum { CH_SCORE = 0, CH_SCORE2 = 1, CH_COMMIT = 2 };
+
+ncclComm *chan_comm(const nas_ctx *ctx, int ch) {
+    return ch == CH_SCORE2 ? ctx->comm2 : ch == CH_COMMIT ? ctx->comm_c : ctx->comm;
+}
+
+// a communicator exchanges even at world 1 (nas_comm_init with world 1
+// builds one: the whole RCCL path on a single GPU, all-gather = copy)
+bool exchanging(const nas_ctx *ctx) { return has_coll(ctx) && !ctx->virtual_shard; }
+
+}  // namespace
+
+// The in-process group: one rendezvous per channel.  An exchange is two
+// host-side barriers.  (1) Every rank records "send ready" on its stream and
+// posts {send buffers, event}; after the barrier each rank makes its stream
+// wait for every peer's event and PULLS all ranks' buffers into its receive
+// buffer with one k_local_gather launch per segment.  (2) Every rank records
+// "copies done" and posts it; after the barrier each stream waits for every
+// peer's copies, so no rank overwrites a send buffer a peer still reads (the
+// completion guarantee an RCCL all-gather gives its caller).  Every stream
+// wait is enqueued after the event it waits on was recorded (the barriers),
+// so streams sharing a hardware queue cannot deadlock.  Events alternate by
+// exchange parity: a rank re-records a parity only after every peer passed the
+// next exchange's first barrier, i.e. finished waiting on it.  A barrier that
+// misses NAS_OPT_COMM_TIMEOUT_MS breaks the group: every rank's pending and
+// later exchanges fail with NAS_ERR_COMM.
+struct nas::LocalGroup {
+    struct Seg {
+        const void *send = nullptr;
+        size_t bytes = 0;
+    };
+    struct Post {
+        Seg seg[2];
+        int nseg = 0;
+        hipEvent_t ev = nullptr;
+        int device = 0;
+    };
+    struct Chan {
+        uint64_t gen = 0;
+        int arrived = 0;
+        std::vector<Post> send, done;
+    };
+    explicit LocalGroup(int w) : world(w), joined(w, false) {
+        for (Chan &c : ch) {
+            c.send.resize(w);
+            c.done.resize(w);
+        }
+    }
+    const int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool broken = false;
+    std::vector<bool> joined;
+    Chan ch[3];
+
+    // under lk; false: timed out or broken (the group is then broken)
+    bool barrier(Chan &c, std::unique_lock<std::mutex> &lk, int64_t timeout_ms) {
+        if (broken) return false;
+        const uint64_t gen = c.gen;
+        if (++c.arrived == world) {
+            c.arrived = 0;
+            ++c.gen;
+            cv.notify_all();
+            return true;
+        }
+        auto passed = [&] { return c.gen != gen || broken; };
+        if (timeout_ms > 0) {
+            if (!cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), passed)) broken = true;
+        } else {
+            cv.wait(lk, passed);
+        }
+        if (c.gen != gen) return true;
+        broken = true;
+        cv.notify_all();
+        return false;
+    }
+    void break_group() {
+        std::lock_guard<std::mutex> g(mu);
+        broken = true;
+        cv.notify_all();
+    }
+};
+
+struct nas_local_group {
+    std::shared_ptr<nas::LocalGroup> g;
+};
+
+namespace {
+
+struct GatherSeg {
+    const void *send;
+    void *recv;
+    size_t bytes;  // per rank; recv holds world * bytes, rank-major
+};
+
+void abort_comms(nas_ctx *ctx);
+
+int local_fail(nas_ctx *ctx, const std::string &what) {
+    abort_comms(ctx);
+    return nas::fail(ctx, NAS_ERR_COMM,
+                     what + " (in-process group): a rank did not join within " +
+                         std::to_string(ctx->opt_comm_timeout_ms) +
+                         " ms (NAS_OPT_COMM_TIMEOUT_MS) or the group is broken; context poisoned");
+}
+
+int local_allgather(nas_ctx *ctx, int ch, hipStream_t st, const GatherSeg *segs, int nseg,
+                    const char *what) {
+    nas::LocalGroup &g = *ctx->local;
+    const int G = g.world, me = ctx->rank;
+    const int par = (int)(ctx->lg_round[ch]++ & 1);
+    hipEvent_t ready = ctx->lg_ev[ch][par][0], copied = ctx->lg_ev[ch][par][1];
+    HIPCK(hipEventRecord(ready, st));
+    std::vector<nas::LocalGroup::Post> peers;
+    nas::LocalGroup::Chan &c = g.ch[ch];
+    {
+        std::unique_lock<std::mutex> lk(g.mu);
+        nas::LocalGroup::Post &p = c.send[me];
+        p.nseg = nseg;
+        for (int s = 0; s < nseg; ++s) p.seg[s] = {segs[s].send, segs[s].bytes};
+        p.ev = ready;
+        p.device = ctx->device;
+        if (!g.barrier(c, lk, ctx->opt_comm_timeout_ms)) {
+            lk.unlock();
+            return local_fail(ctx, what);
+        }
+        peers = c.send;
+    }
+    for (int j = 0; j < G; ++j) {
+        bool same = peers[j].nseg == nseg;
+        for (int s = 0; same && s < nseg; ++s) same = peers[j].seg[s].bytes == segs[s].bytes;
+        if (!same) {
+            g.break_group();
+            return local_fail(ctx, std::string(what) + ": ranks issued different exchanges");
+        }
+        if (j == me) continue;
+        HIPCK(hipStreamWaitEvent(st, peers[j].ev, 0));
+        const int pd = peers[j].device;
+        if (pd != ctx->device && !(ctx->lg_peers >> (pd & 63) & 1)) {
+            const hipError_t e = hipDeviceEnablePeerAccess(pd, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                return nas::hip_fail(ctx, e, "hipDeviceEnablePeerAccess");
+            (void)hipGetLastError();
+            ctx->lg_peers |= 1ull << (pd & 63);
+        }
+    }
+    for (int s = 0; s < nseg; ++s) {
+        nas::LocalSrcs src{};
+        for (int j = 0; j < G; ++j) src.p[j] = peers[j].seg[s].send;
+        HIPCK(nas::launch_local_gather(st, src, G, segs[s].recv, segs[s].bytes));
+    }
+    HIPCK(hipEventRecord(copied, st));
+    {
+        std::unique_lock<std::mutex> lk(g.mu);
+        c.done[me].ev = copied;
+        if (!g.barrier(c, lk, ctx->opt_comm_timeout_ms)) {
+            lk.unlock();
+            return local_fail(ctx, what);
+        }
+        peers = c.done;
+    }
+    for (int j = 0; j < G; ++j)
+        if (j != me) HIPCK(hipStreamWaitEvent(st, peers[j].ev, 0));
+    return NAS_OK;
+}
+
+// all-gather of nseg (<= 2) segments on channel ch, stream st: each rank's
+// segs[s].send (bytes each, a multiple of 8) into segs[s].recv [world][bytes]
+int allgather(nas_ctx *ctx, int ch, hipStream_t st, const GatherSeg *segs, int nseg,
+              const char *what) {
+    if (ctx->local) return local_allgather(ctx, ch, st, segs, nseg, what);
+    ncclComm *cm = chan_comm(ctx, ch);
     auto comm = reinterpret_cast<ncclComm_t>(cm);
-    ncclResult_t r = ncclGroupStart();
-    if (r == ncclSuccess) r = ncclAllGather(keys, gk, np * KC, ncclUint64, comm, st);
-    if (r == ncclSuccess) r = ncclAllGather(bounds, gb, np, ncclUint64, comm, st);
-    ncclResult_t r2 = ncclGroupEnd();
-    if (r == ncclSuccess) r = r2;
-    OK(nccl_enqueued(ctx, cm, r, "ncclAllGather"));
+    ncclResult_t r = nseg > 1 ? ncclGroupStart() : ncclSuccess;
+    for (int s = 0; s < nseg && r == ncclSuccess; ++s)
+        r = ncclAllGather(segs[s].send, segs[s].recv, segs[s].bytes / 8, ncclUint64, comm, st);
+    if (nseg > 1) {
+        const ncclResult_t r2 = ncclGroupEnd();
+        if (r == ncclSuccess) r = r2;
+    }
+    return nccl_enqueued(ctx, cm, r, what);
+}
+
+// all-gather each rank's per-pod lists (keys [np][KC] + bounds [np]) into
+// gk [world][np][KC] / gb [world][np] on `st` over channel ch
+int exchange(nas_ctx *ctx, int ch, hipStream_t st, const uint64_t *keys, const uint64_t *bounds,
+             size_t np, uint64_t *gk, uint64_t *gb) {
+    const GatherSeg segs[2] = {{keys, gk, np * KC * 8}, {bounds, gb, np * 8}};
+    OK(allgather(ctx, ch, st, segs, 2, "ncclAllGather"));
     if (ctx->rehearse > 1) {
         HIPCK(nas::launch_rehearse_replicate(st, gk, np * KC, ctx->rehearse, ctx->N));
         HIPCK(nas::launch_rehearse_replicate(st, gb, np, ctx->rehearse, ctx->N));
     }
     return NAS_OK;
 }
-
-// a communicator exchanges even at world 1 (nas_comm_init with world 1
-// builds one: the whole RCCL path on a single GPU, all-gather = copy)
-bool exchanging(const nas_ctx *ctx) { return ctx->comm != nullptr && !ctx->virtual_shard; }
 
 // The pod arrays a scoring pass reads and writes: the context's own, or the
 // gathered scratch view of a rescore (k_rescore.hip) with its own row stride.
@@ -468,7 +649,7 @@ PodView main_view(nas_ctx *ctx) {
 // merge of pods [p_lo, p_hi)'s node-tile lists (-> exchange over `cm` and
 // merge across ranks), on stream st behind their cost launch; gbuf picks the
 // gathered-list scratch (one per stream that exchanges)
-int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, ncclComm *cm,
+int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, int ch,
                 int gbuf, const PodView &v) {
     const int pr0 = p_lo / nas::COST_BN * nas::COST_BN;
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
@@ -490,8 +671,8 @@ int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, ncc
         HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
                                 n_lists, (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, xs,
                                 xs + (size_t)np * KC, pr0));
-        ncclResult_t r = ncclAllGather(xs, gx, seg, ncclUint64, reinterpret_cast<ncclComm_t>(cm), st);
-        OK(nccl_enqueued(ctx, cm, r, "ncclAllGather"));
+        const GatherSeg g1{xs, gx, seg * 8};
+        OK(allgather(ctx, ch, st, &g1, 1, "ncclAllGather"));
         if (ctx->rehearse > 1)
             HIPCK(nas::launch_rehearse_replicate(st, gx, seg, ctx->rehearse, ctx->N));
         HIPCK(nas::launch_merge(st, gx, gx + (size_t)np * KC, ctx->world, (int64_t)seg,
@@ -537,7 +718,7 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
     ctx->timings.cost_launches += 1;
-    if (merge) OK(merge_range(ctx, tm, p_lo, p_hi, st, sidx ? ctx->comm2 : ctx->comm, sidx, v));
+    if (merge) OK(merge_range(ctx, tm, p_lo, p_hi, st, sidx ? CH_SCORE2 : CH_SCORE, sidx, v));
     return NAS_OK;
 }
 
@@ -550,7 +731,7 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
 // kernel exits at once (the exchange still runs, so all ranks issue the same
 // collectives).  Slots need no host round trip, so a crowded cluster's many
 // stops cost launches, not synchronisations.
-int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t *pub, int hi) {
+int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, int ch, int32_t *pub, int hi) {
     const int R = std::min(GATHER_PODS, ctx->Pp);
     OK(nas::ensure(ctx, ctx->g_words, (size_t)nas::stale_words(ctx->Pp) * 8));
     OK(nas::ensure(ctx, ctx->g_idx, (size_t)R * 4));
@@ -588,7 +769,7 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, ncclComm *cm, int32_t
         OK(nas::ensure(ctx, ctx->g_gb, (size_t)ctx->world * R * 8));
         auto *xk = ctx->g_gk.as<uint64_t>();
         auto *xb = ctx->g_gb.as<uint64_t>();
-        OK(exchange(ctx, cm, st, gk, gb, (size_t)R, xk, xb));
+        OK(exchange(ctx, ch, st, gk, gb, (size_t)R, xk, xb));
         HIPCK(nas::launch_merge(st, xk, xb, ctx->world, (int64_t)R * KC, R, 0, 0, 0, ck, cbnd, 0,
                                 &dyn, 0, 1, 0, idx));
     }
@@ -643,7 +824,7 @@ int rescore_slot(nas_ctx *ctx, hipStream_t sc, int hi, int32_t *pub = nullptr) {
         HIPCK(nas::launch_merge(sc, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
                                 n_lists, (int64_t)ctx->Pp * KC, ctx->Pp, 0, 0, 0, rk, rb, 0, &dyn,
                                 nas::MERGE_DST_WINDOW));
-        OK(exchange(ctx, ctx->comm_c, sc, rk, rb, RESCORE_PODS, gk, gb));
+        OK(exchange(ctx, CH_COMMIT, sc, rk, rb, RESCORE_PODS, gk, gb));
         HIPCK(nas::launch_merge(sc, gk, gb, ctx->world, (int64_t)RESCORE_PODS * KC, RESCORE_PODS,
                                 0, 0, 0, ctx->cand_key.as<uint64_t>(),
                                 ctx->cand_bound.as<uint64_t>(), 0, &dyn, nas::MERGE_SRC_WINDOW));
@@ -782,6 +963,8 @@ void abort_comms(nas_ctx *ctx) {
         if (*c) (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(*c));
         *c = nullptr;
     }
+    // in-process group: every peer's pending and later exchanges fail too
+    if (ctx->local) ctx->local->break_group();
     ctx->poisoned = true;
 }
 
@@ -792,7 +975,7 @@ void abort_comms(nas_ctx *ctx) {
 // communicators and poison the context.  (Polling measured equal to the
 // blocking wait on the G = 8 rehearsal: 1.38-1.41 ms per pass either way.)
 int wait_event(nas_ctx *ctx, hipEvent_t e) {
-    if (!ctx->comm || ctx->opt_comm_timeout_ms <= 0) {
+    if (!has_coll(ctx) || ctx->opt_comm_timeout_ms <= 0) {
         HIPCK(hipEventSynchronize(e));
         return NAS_OK;
     }
@@ -819,7 +1002,7 @@ int wait_event(nas_ctx *ctx, hipEvent_t e) {
 
 // stream synchronisation of the calls that may have issued collectives
 int sync_stream(nas_ctx *ctx, hipStream_t st) {
-    if (!ctx->comm) {
+    if (!has_coll(ctx)) {
         HIPCK(hipStreamSynchronize(st));
         return NAS_OK;
     }
@@ -1078,6 +1261,21 @@ void destroy_comms(nas_ctx *ctx) {
     // children use (no splitShare): aborting it needs no peer
     if (ctx->comm_root) (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(ctx->comm_root));
     ctx->comm_root = nullptr;
+    // in-process group: give the rank back (callers synchronised the streams
+    // that waited on the events)
+    if (ctx->local) {
+        {
+            std::lock_guard<std::mutex> g(ctx->local->mu);
+            ctx->local->joined[ctx->rank] = false;
+        }
+        ctx->local.reset();
+        for (auto &c : ctx->lg_ev)
+            for (auto &p : c)
+                for (hipEvent_t &e : p) {
+                    if (e) (void)hipEventDestroy(e);
+                    e = nullptr;
+                }
+    }
 }
 
 }  // namespace
@@ -1165,7 +1363,7 @@ int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value) {
         return NAS_OK;
     case NAS_OPT_REHEARSE_WORLD:
         if (value < 0 || value > 64) break;
-        if (ctx->comm) return nas::fail(ctx, NAS_ERR_STATE, "set NAS_OPT_REHEARSE_WORLD before nas_comm_init");
+        if (has_coll(ctx)) return nas::fail(ctx, NAS_ERR_STATE, "set NAS_OPT_REHEARSE_WORLD before nas_comm_init");
         ctx->opt_rehearse_world = (int32_t)value;
         return NAS_OK;
     case NAS_OPT_INJECT_STALL_MS:
@@ -1382,9 +1580,8 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
         OK(nas::ensure(ctx, ctx->vote_gather, rb * ranks));
         HIPCK(nas::launch_vote_partial(ctx->stream, ctx, Sused, ctx->vote_part.as<nas_vote_partial>()));
         b = tm.mark();  // vote_ms: the slice's HBM pass alone
-        ncclResult_t r = ncclAllGather(ctx->vote_part.p, ctx->vote_gather.p, rb, ncclUint8,
-                                       reinterpret_cast<ncclComm_t>(ctx->comm), ctx->stream);
-        OK(nccl_enqueued(ctx, ctx->comm, r, "vote all-gather"));
+        const GatherSeg g1{ctx->vote_part.p, ctx->vote_gather.p, rb};
+        OK(allgather(ctx, CH_SCORE, ctx->stream, &g1, 1, "vote all-gather"));
         HIPCK(nas::launch_vote_merge(ctx->stream, ctx, ctx->vote_gather.as<nas_vote_partial>(),
                                      ranks, Sused, ctx->snap_best.as<int32_t>(),
                                      ctx->snap_win.as<int32_t>()));
@@ -1418,7 +1615,7 @@ int nas_score_reference(nas_ctx *ctx, const int32_t *order1, const int32_t *orde
     HIPCK(hipMemcpyAsync(stage, best_d, (size_t)P * 4, hipMemcpyDeviceToHost, ctx->stream));
     if (winners_out)
         HIPCK(hipMemcpyAsync(stage + P, win_d, (size_t)P * 24, hipMemcpyDeviceToHost, ctx->stream));
-    if (ctx->snap_sharded && ctx->comm) inject_stall(ctx, ctx->stream);
+    if (ctx->snap_sharded && has_coll(ctx)) inject_stall(ctx, ctx->stream);
     hipEvent_t c = tm.mark();
     if (ctx->snap_sharded) OK(sync_stream(ctx, ctx->stream));
     else HIPCK(hipStreamSynchronize(ctx->stream));
@@ -1831,7 +2028,7 @@ int nas_score(nas_ctx *ctx) {
     Timer tm(ctx);
     if (ctx->B > 1) OK(score_batch(ctx, tm));
     else OK(score_range(ctx, tm, 0, ctx->P));
-    if (ctx->comm) inject_stall(ctx, ctx->stream);
+    if (has_coll(ctx)) inject_stall(ctx, ctx->stream);
     OK(sync_stream(ctx, ctx->stream));
     ctx->timings.fit_ms = tm.total(T_FIT);
     ctx->timings.cost_ms = tm.total(T_COST);
@@ -1894,7 +2091,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // merge / commit / copies stay on the scoring stream, which saves the
     // cross-stream event hops (~15-20 us each) that dominate a small pass
     // (C1 extended 0.41 -> 0.385 ms per nas_place)
-    const bool one_stream = chunks.size() == 1 && !ctx->comm;
+    const bool one_stream = chunks.size() == 1 && !has_coll(ctx);
     if (one_stream) sc = st;
     // With the LDS commit nothing the scoring kernels read comes from the
     // pass init (capacity is read live), so the first chunk's fit and cost are
@@ -1942,7 +2139,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         } else {
             HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
         }
-        OK(merge_range(ctx, tm, lo, hi, cs, ctx->comm_c, 0, main_view(ctx)));
+        OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx)));
         hipEvent_t c0 = tm.fine(cs);
         HIPCK(nas::launch_commit(cs, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
@@ -1958,13 +2155,13 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // when the last chunk ran on another stream
     if (!one_stream && ss2[(chunks.size() - 1) & 1] != st)
         HIPCK(hipStreamWaitEvent(st, tm.mark(ss2[(chunks.size() - 1) & 1]), 0));
-    if (ctx->comm) inject_stall(ctx, st);  // behind every collective of the pass
+    if (has_coll(ctx)) inject_stall(ctx, st);  // behind every collective of the pass
     // speculative slots: as many as the previous pass of this shape needed
     // (consecutive passes over similar clusters stop alike), enqueued before
     // the first status round trip; a slot whose walk is not halted exits at
     // once.  Not with a communicator: every rank must issue the same slots.
-    const int spec = (!ctx->comm && ctx->slot_hint_P == P && ctx->slot_hint_N == N) ? ctx->slot_hint : 0;
-    for (int r = 0; r < spec; ++r) OK(gathered_slot(ctx, tm, st, nullptr, nullptr, P));
+    const int spec = (!has_coll(ctx) && ctx->slot_hint_P == P && ctx->slot_hint_N == N) ? ctx->slot_hint : 0;
+    for (int r = 0; r < spec; ++r) OK(gathered_slot(ctx, tm, st, CH_SCORE, nullptr, P));
     if (spec > 0) {
         // behind the slots, all placements again: when they finished the walk,
         // the status round trip below brings the final results with it
@@ -2026,7 +2223,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         if (hs[0] >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
         if (++checks > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
         for (int r = 0, n = gather_batch(checks); r < n; ++r)
-            OK(gathered_slot(ctx, tm, st, ctx->comm, nullptr, P));
+            OK(gathered_slot(ctx, tm, st, CH_SCORE, nullptr, P));
         OK(fetch());
         if (hs[0] < 0) {
             unsched = 0;
@@ -2097,7 +2294,7 @@ int nas_score_range(nas_ctx *ctx, int32_t p_lo, int32_t p_hi) {
     std::memset(&ctx->timings, 0, sizeof(ctx->timings));
     Timer tm(ctx);
     OK(score_range(ctx, tm, p_lo, p_hi));
-    if (ctx->comm) inject_stall(ctx, ctx->stream);
+    if (has_coll(ctx)) inject_stall(ctx, ctx->stream);
     OK(sync_stream(ctx, ctx->stream));
     ctx->timings.fit_ms = tm.total(T_FIT);
     ctx->timings.cost_ms = tm.total(T_COST);
@@ -2235,8 +2432,13 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     if (ctx->B > 1 && world > 1)
         return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");
     destroy_comms(ctx);
-    // on any failure below the context keeps its previous geometry (a context
-    // left at world > 1 without communicators would place from its own shard)
+    // the previous communicators are gone: until this call succeeds the
+    // context is a single rank (a context left at world > 1 without
+    // communicators would fail every sharded call with a null communicator)
+    ctx->rank = 0;
+    ctx->world = 1;
+    ctx->rehearse = 0;
+    ctx->virtual_shard = false;
     int32_t eff_world = world, rehearse = 0;
     if (ctx->opt_rehearse_world > 1 && world == 1) {
         // diagnostic (NAS_OPT_REHEARSE_WORLD): one rank of a G-GPU pass
@@ -2455,12 +2657,66 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     return NAS_OK;
 }
 
+int nas_local_group_create(int32_t world, nas_local_group **out) {
+    NAS_RANGE("nas_local_group_create");
+    if (!out) return NAS_ERR_ARG;
+    *out = nullptr;
+    if (world < 1 || world > nas::LOCAL_MAX_WORLD) return NAS_ERR_ARG;
+    auto *g = new (std::nothrow) nas_local_group();
+    if (!g) return NAS_ERR_NOMEM;
+    g->g = std::make_shared<nas::LocalGroup>(world);
+    *out = g;
+    return NAS_OK;
+}
+
+void nas_local_group_destroy(nas_local_group *g) {
+    NAS_RANGE("nas_local_group_destroy");
+    delete g;
+}
+
+int nas_comm_init_local(nas_ctx *ctx, nas_local_group *group, int32_t rank) {
+    NAS_RANGE("nas_comm_init_local");
+    OK(bind(ctx));
+    if (!group || !group->g) return nas::fail(ctx, NAS_ERR_ARG, "nas_comm_init_local: group");
+    const int world = group->g->world;
+    if (rank < 0 || rank >= world) return nas::fail(ctx, NAS_ERR_ARG, "nas_comm_init_local: rank");
+    if (ctx->have_L || ctx->have_wa || ctx->have_cap)
+        return nas::fail(ctx, NAS_ERR_STATE, "nas_comm_init_local must precede the extended uploads");
+    if (ctx->B > 1 && world > 1)
+        return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");
+    destroy_comms(ctx);
+    ctx->rank = 0;
+    ctx->world = 1;
+    ctx->rehearse = 0;
+    ctx->virtual_shard = false;
+    {
+        std::lock_guard<std::mutex> g(group->g->mu);
+        if (group->g->broken) return nas::fail(ctx, NAS_ERR_COMM, "nas_comm_init_local: group is broken");
+        if (group->g->joined[rank])
+            return nas::fail(ctx, NAS_ERR_STATE, "nas_comm_init_local: rank already joined");
+        group->g->joined[rank] = true;
+    }
+    ctx->local = group->g;
+    for (auto &c : ctx->lg_ev)
+        for (auto &p : c)
+            for (hipEvent_t &e : p)
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+                    destroy_comms(ctx);
+                    return nas::fail(ctx, NAS_ERR_HIP, "nas_comm_init_local: hipEventCreate");
+                }
+    for (uint32_t &r : ctx->lg_round) r = 0;
+    ctx->lg_peers = 0;
+    ctx->rank = rank;
+    ctx->world = world;
+    return NAS_OK;
+}
+
 int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world) {
     NAS_RANGE("nas_set_shard");
     OK(bind(ctx));
     if (world < 1 || rank < 0 || rank >= world)
         return nas::fail(ctx, NAS_ERR_ARG, "nas_set_shard: rank/world");
-    if (ctx->comm) return nas::fail(ctx, NAS_ERR_STATE, "context already has a communicator");
+    if (has_coll(ctx)) return nas::fail(ctx, NAS_ERR_STATE, "context already has a communicator");
     if (ctx->have_L || ctx->have_wa || ctx->have_cap)
         return nas::fail(ctx, NAS_ERR_STATE, "nas_set_shard must precede the extended uploads");
     if (ctx->B > 1 && world > 1)

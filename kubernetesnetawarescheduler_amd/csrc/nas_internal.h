@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <atomic>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -74,6 +75,16 @@ struct Ovf {
     const int32_t *row_count = nullptr;
     int N = 0;  // rows of one cluster's Lr
 };
+
+// In-process transport (nas_comm_init_local): G contexts of one process, each
+// driven by its own host thread, exchange candidate lists through device
+// memory instead of RCCL.  Kernel argument of k_local_gather: the G ranks'
+// send buffers of one exchange.
+constexpr int LOCAL_MAX_WORLD = 64;
+struct LocalSrcs {
+    const void *p[LOCAL_MAX_WORLD];
+};
+struct LocalGroup;  // nas_api.hip
 
 }  // namespace nas
 
@@ -172,6 +183,14 @@ struct nas_ctx {
     // a G-GPU pass on a single GPU; placements are not meaningful
     int32_t rehearse = 0;
     bool virtual_shard = false;  // nas_set_shard: shard geometry, no exchange
+    // in-process transport instead of RCCL (nas_comm_init_local): the group,
+    // per channel (0 = scoring stream, 1 = scoring stream 2, 2 = commit
+    // stream) the exchange count and two events per parity {send ready, copies
+    // done}, and the peer devices this context already reads from
+    std::shared_ptr<nas::LocalGroup> local;
+    uint32_t lg_round[3] = {0, 0, 0};
+    hipEvent_t lg_ev[3][2][2] = {};
+    uint64_t lg_peers = 0;
     // options (nas_set_option)
     bool opt_stage_timings = true;
     int64_t opt_comm_timeout_ms = 120000;
@@ -286,6 +305,10 @@ hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap,
 // (or bounds) = slot 0 with node indices shifted to rank r's first node
 // (r * N / G); ~0 stays
 hipError_t launch_rehearse_replicate(hipStream_t st, uint64_t *buf, size_t n, int G, int N);
+// in-process all-gather (nas_comm_init_local): dst[r * bytes ..] = srcs.p[r][0 .. bytes)
+// for r < G (bytes a multiple of 8), on the receiving rank's stream
+hipError_t launch_local_gather(hipStream_t st, const LocalSrcs &srcs, int G, void *dst,
+                               size_t bytes);
 hipError_t launch_transpose_L(hipStream_t st, const void *L_dev, int dtype, int N, int n0,
                               int nloc, int Mp, int Kp, void *Lt);
 // bf16 CSR traffic -> dense WA rows (fp32 sums, rounded once)

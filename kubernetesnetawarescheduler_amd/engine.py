@@ -19,6 +19,55 @@ _FDT = {"cpu": np.float64, "mem": np.float64, "rx": np.int64, "tx": np.int64,
         "bw": np.float64, "disk": np.int64}
 
 
+class LocalGroup:
+    """nas_local_group: `world` Engines of this process that exchange like
+    RCCL ranks.  Each rank's calls must run on their own thread (ctypes
+    releases the GIL inside them); see local_ranks()."""
+
+    def __init__(self, world):
+        self._L = _lib.lib()
+        h = ctypes.c_void_p()
+        rc = self._L.nas_local_group_create(world, ctypes.byref(h))
+        if rc != 0:
+            raise NasError(rc, "nas_local_group_create: world out of range")
+        self.handle = h
+        self.world = world
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._L.nas_local_group_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+def local_ranks(engines, fn):
+    """Run fn(rank, engine) for every rank of an in-process group concurrently
+    (one thread each, as the group's barriers require); returns the results in
+    rank order and re-raises the first rank's exception."""
+    import threading
+
+    out = [None] * len(engines)
+    err = [None] * len(engines)
+
+    def run(r):
+        try:
+            out[r] = fn(r, engines[r])
+        except BaseException as ex:  # noqa: BLE001 -- re-raised below
+            err[r] = ex
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(len(engines))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for ex in err:
+        if ex is not None:
+            raise ex
+    return out
+
+
 class Engine:
     def __init__(self, device=0):
         self._L = _lib.lib()
@@ -163,6 +212,13 @@ class Engine:
     def comm_init(self, uid, rank, world):
         b = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
         self._ck(self._L.nas_comm_init(self._h, b, rank, world))
+        self.has_comm = True
+
+    def comm_init_local(self, group, rank):
+        """Join an in-process group (LocalGroup) as `rank` (include/nas.h
+        nas_comm_init_local): node shard of group.world ranks whose
+        exchanges run device to device instead of over RCCL."""
+        self._ck(self._L.nas_comm_init_local(self._h, group.handle, rank))
         self.has_comm = True
 
     def set_shard(self, rank, world):

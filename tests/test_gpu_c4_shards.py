@@ -60,3 +60,29 @@ def test_c4_virtual_shards_equal_world1(world1, G):
     used = np.zeros((N, 3), np.int64)
     np.add.at(used, node[placed], req[placed].astype(np.int64))
     assert (cap0.astype(np.int64) - used == free1).all() and (free1 >= 0).all()
+
+
+def test_c4_local_group_g2_equals_world1(world1):
+    """C4 as 2 in-process ranks (nas_comm_init_local): the
+    device exchange path of nas_place -- per-chunk all-gather of distinct
+    rank lists into [2][np][8 + 1], the cross-rank k_merge, the replicated L2
+    commit -- at the full 50k x 500k size, equal to world 1."""
+    from kubernetesnetawarescheduler_amd import LocalGroup, local_ranks
+    node1, score1, free1, _, _ = world1
+    group = LocalGroup(2)
+    engines = [Engine(0) for _ in range(2)]
+    try:
+        def run(r, e):
+            e.comm_init_local(group, r)
+            e.synth_cluster(SEED, N, P, "i8", peers=8)
+            node, _, score = e.place()
+            return node, score, e.get_capacity()
+        res = local_ranks(engines, run)
+    finally:
+        for e in engines:
+            e.close()
+        group.close()
+    for r, (node, score, cap) in enumerate(res):
+        bad = np.nonzero(node != node1)[0]
+        assert len(bad) == 0, (r, bad[:8], node[bad[:8]], node1[bad[:8]])
+        assert (score == score1).all() and (cap == free1).all(), r
