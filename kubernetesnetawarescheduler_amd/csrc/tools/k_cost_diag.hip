@@ -1,3 +1,12 @@
+// k_cost_diag.hip -- DIAGNOSTIC ONLY (included by tools/mb_cost.hip and
+// tools/mb_aux.hip, never built into libnas.so): the round-3 cost kernel
+// with every measured-and-rejected variant of DESIGN.md §4 still selectable
+// -- PIPE 1-7 (triple-buffered B, register staging, phased / staggered loops,
+// L2 touches), SCHED 1-5 (pinned MFMA / ds_read interleaves, setprio,
+// iglp_opt), NWN = 2 (one wave per SIMD), EPI 1-6 (main loop alone, top-1,
+// exact select network, all-L2-hit and LDS-only ceilings), COST_AUX cache
+// policies and the early overflow seeding.  The product kernel
+// (../k_cost.hip) keeps only the shipped configuration.
 // k_cost.hip -- network cost contraction on gfx950 MFMA with a fused
 // fit-mask + per-pod top-k epilogue.
 //
@@ -29,7 +38,7 @@
 // registers -> merged with lane^32 into an 8-list with an exactness bound
 // (klist.h) -> merged across the two node-half waves through LDS ->
 // partial[node_tile][pod][8] + pbound[node_tile][pod] (72 B per pod per tile).
-#include "klist.h"
+#include "../klist.h"
 
 #include <type_traits>
 
@@ -41,28 +50,80 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+[[maybe_unused]] constexpr int THREADS = 512;  // the default (NWN = 4) workgroup, for tools/
 constexpr int BM = COST_BM;   // nodes per tile
 constexpr int BN = COST_BN;   // pods per tile
 constexpr int BKB = COST_BKB; // bytes of K per LDS stage (full 128-byte lines)
-// XCD tile order, pod-group major: PG pod tiles x every node tile per group,
-// so an XCD keeps one pod group's traffic rows hot in the memory-side cache
-// while it sweeps the node tiles.  256 x 256: groups of 4 (32 concurrent
-// workgroups per XCD = 8 node tiles x 4 pod tiles), 2.0-2.5% faster than
-// node-group-major 4 (profiles/r02_mb_cost_order.log); the wide tile: groups
-// of 2, C3 pass 8.04-8.09 vs 8.09-8.12 ms for groups of 4 (launch equal;
-// groups of 1 / 3 / 8 and node-group-major 2 / 8 slower,
-// profiles/r02_s4_ab_gm.txt, r03_ab_gm_wide.txt).  The measured-and-rejected
-// variants of this kernel (other pipelines, schedules, one wave per SIMD,
-// cache policies) live in tools/k_cost_diag.hip.
-constexpr int PG_NARROW = 4;
-constexpr int PG_WIDE = 2;
-// wave layouts: NWN = 4 -> 256 x 256 per 8-wave workgroup (2 node halves x 4
-// pod quarters, each wave 128 nodes x 64 pods = 4 x 2 MFMA 32x32 tiles, 128
-// accumulator registers, two waves per SIMD, 128 KiB LDS double buffer);
-// NWN = 6 -> the wide tile, 256 x 384 per 12-wave workgroup (3 waves per
-// SIMD of the same 128 x 64 shape, 160 KiB LDS double buffer), 17% fewer
-// staged bytes per MAC, for the main scoring pass of one large cluster
-constexpr int WIDE_PODS = 384;
+constexpr int STAGE_BYTES = (BM + BN) * BKB;  // 64 KiB
+constexpr int TILE_BYTES = BM * BKB;          // 32 KiB: one operand, one stage
+#ifndef COST_PIPE
+#define COST_PIPE 0
+#endif
+// XCD tile order: GM > 0 = node-group major (GM node tiles x every pod tile);
+// GM = -PG = pod-group major (PG pod tiles x every node tile).  Pod groups of
+// 4 (32 concurrent workgroups per XCD = 8 node tiles x 4 pod tiles) fetch
+// fewer traffic rows from HBM per window and more latency rows from the
+// Infinity Cache (Lt, 105 MB, fits it): 2.0-2.5% faster than GM = 4 in 4 of 4
+// interleaved repetitions (profiles/r02_mb_cost_order.log)
+#ifndef COST_GM
+#define COST_GM (-4)
+#endif
+// the wide tile's order: pod groups of 2 (2 x 384 pods x every node tile):
+// C3 pass 8.04-8.09 vs 8.09-8.12 ms for groups of 4 (launch equal), groups
+// of 1 / 3 / 8 and node-group-major 2 / 8 slower (profiles/r02_s4_ab_gm.txt)
+#ifndef COST_GM_WIDE
+#define COST_GM_WIDE (-2)
+#endif
+// PIPE 0: A and B double-buffered (128 KiB).  PIPE 1: A (latency rows, mostly
+// L2/MALL-resident) double-buffered, B (the 1 GB traffic stream, mostly HBM)
+// triple-buffered so its loads get two K-steps of cover (160 KiB, all of LDS).
+// PIPE 2: as 0, but B is staged through registers (global_load_dwordx4 ->
+// ds_write_b128) instead of LDS-DMA; PIPE 3: both operands register-staged.
+// PIPE 5 / 6: as 0, plus an L2 "touch" of the stage 2 / 3 K-steps ahead (one
+// 4-byte LDS-DMA per 128-byte line of A and B into a junk LDS word, left in
+// flight across the step's barrier), so the stage's own LDS-DMA one step
+// later hits L2 instead of waiting on HBM / MALL; PIPE 7: as 5, B lines only.
+template <int PIPE>
+constexpr int lds_bytes() {
+    return PIPE == 1 ? 5 * TILE_BYTES : PIPE >= 5 ? 2 * STAGE_BYTES + 256 : 2 * STAGE_BYTES;
+}
+#ifndef COST_SCHED
+#define COST_SCHED 0
+#endif
+// wave layout of the 256 x 256 tile: NWN = 4 -> 8 waves (2 node halves x 4 pod
+// quarters), each 128 nodes x 64 pods (4 x 2 MFMA tiles, 128 accumulator
+// registers, two waves per SIMD); NWN = 2 -> 4 waves (2 x 2), each 128 nodes x
+// 128 pods (4 x 4 tiles, 256 accumulator registers, one wave per SIMD): half
+// the LDS fragment reads per MFMA (the layout hipBLASLt picks for this shape,
+// MT256x256, 4 waves; profiles/r02_s3_vendor_gemm_kernels.txt)
+#ifndef COST_NWN_I8
+#define COST_NWN_I8 4
+#endif
+#ifndef COST_NWN_BF16
+#define COST_NWN_BF16 4
+#endif
+template <int DT>
+constexpr int cost_nwn() {
+    return DT == NAS_DT_I8 ? COST_NWN_I8 : COST_NWN_BF16;
+}
+// the main scoring pass (no rescore window) on the wide tile: 256 nodes x
+// 384 pods per 12-wave workgroup (3 waves per SIMD, each 128 x 64 as in the
+// 8-wave layout, 160 KiB of LDS double buffer), 17% fewer staged bytes per
+// MAC than 256 x 256
+#ifndef COST_WIDE_I8
+#define COST_WIDE_I8 1
+#endif
+#ifndef COST_WIDE_BF16
+#define COST_WIDE_BF16 1
+#endif
+template <int DT>
+constexpr bool cost_wide() {
+    return DT == NAS_DT_I8 ? COST_WIDE_I8 : COST_WIDE_BF16;
+}
+
+#ifndef COST_OVF_EARLY
+#define COST_OVF_EARLY 0
+#endif
 
 template <int DT>
 struct Mma;
@@ -90,11 +151,20 @@ struct Mma<NAS_DT_BF16> {
     }
 };
 
-// 16-byte LDS-DMA (global_load_lds_dwordx4), default cache policy (sc1,
-// sc0 sc1 measured equal; nt slower: tools/k_cost_diag.hip COST_AUX_*)
+// cache policy of the LDS-DMA loads per operand (build-time knob for
+// tools/mb_aux.hip; gfx950 CPol bits: 1 sc0, 2 nt, 16 sc1).  Measured round 2
+// (same box, alternating): sc1 / sc0 sc1 equal to the default within 1%, nt
+// on the traffic rows +5%, on both operands +15-30% -- default kept.
+#ifndef COST_AUX_A
+#define COST_AUX_A 0
+#endif
+#ifndef COST_AUX_B
+#define COST_AUX_B 0
+#endif
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void *g, void *l) {
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)g,
-                                     (void __attribute__((address_space(3))) *)l, 16, 0, 0);
+                                     (void __attribute__((address_space(3))) *)l, 16, 0, AUX);
 }
 
 __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
@@ -125,30 +195,36 @@ struct Top4 {
     __device__ __forceinline__ u64 key(int j) const { return ((u64)c[j] << 32) | n[j]; }
 };
 
-// Instantiations (launch_cost_t): NWN = 4 (256 x 256) with the k_fit mask
-// (node shards, rescore windows), with the fused fit (FUSE: main pod ranges at
-// world 1, batches) or with a row map (RMAP); NWN = 6 (the wide tile, always
-// fused).  The k-substep schedule is hipcc's own (pinned interleaves,
-// setprio and iglp_opt measured within +-1%: tools/k_cost_diag.hip SCHED).
+// EPI != 0 are diagnostic variants for tools/mb_cost.hip: 1 = accumulators
+// kept alive with an empty asm and no epilogue (times the main loop alone),
+// 2 = per-lane top-1 instead of top-4, 6 = the exact Top4 select network
+// only (the default takes the packed med3 path whenever every lane's keys
+// span < 2^26 - 1).  SCHED selects the k-substep schedule
+// (A/B'd in tools/mb_cost.hip and on the C3 bench): 0 hipcc's own (the
+// default: ~1% ahead of 1 on the bench, 3 of 3 pairs), 1 pinned MFMA/ds_read
+// interleave, 2 s_setprio(1) around each MFMA cluster, 3 iglp_opt(0),
+// 4 iglp_opt(1).
 // RMAP: a gathered rescore view -- view row q's traffic is WA row rowmap[q]
 // (read in place by the LDS-DMA source addresses; rows past the view's count
 // read its last row and are never merged)
-template <int DT, bool RMAP, int NWN, bool FUSE>
+template <int DT, int EPI = 0, int SCHED = COST_SCHED, int PIPE = COST_PIPE, int GM = COST_GM,
+          bool RMAP = false, int NWN = 4, bool FUSE = (NWN == 6)>
 __global__ void __launch_bounds__(128 * NWN, 1)
 k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restrict__ WA, int Kb,
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
             u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base,
             const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
             Ovf ov, const int *__restrict__ rowmap, FitSrc fs) {
-    static_assert(NWN == 4 || NWN == 6, "the 8- and 12-wave layouts");
-    static_assert(NWN != 6 || (!RMAP && FUSE), "the wide tile serves the main pass only");
-    static_assert(!FUSE || !RMAP, "the fused fit: main-range launches");
+    static_assert(!RMAP || PIPE == 0, "the row map is wired into the LDS-DMA staging only");
+    static_assert(NWN == 4 || ((NWN == 2 || NWN == 6) && PIPE == 0 && (SCHED == 0 || SCHED == 2)),
+                  "the 4- and 12-wave layouts have the two-stage LDS-DMA pipeline only");
+    static_assert(NWN != 6 || (!RMAP && EPI == 0 && FUSE), "the wide tile serves the main pass only");
+    static_assert(!FUSE || (!RMAP && EPI == 0 && PIPE == 0), "the fused fit: main-range launches");
     constexpr int NW = 2 * NWN;              // waves
-    constexpr int NI = 2;                    // 32-pod MFMA tiles per wave
+    constexpr int NI = NWN == 2 ? 4 : 2;     // 32-pod MFMA tiles per wave
     constexpr int WPODS = 32 * NI;           // pods per wave
     constexpr int BNK = NWN * WPODS;         // pods per tile (256; the wide tile 384)
-    constexpr int STG = (BM + BNK) * BKB;    // bytes per LDS stage
-    constexpr int PG = NWN == 6 ? PG_WIDE : PG_NARROW;
+    constexpr int STG = (BM + BNK) * BKB;    // bytes per LDS stage (PIPE 0)
     constexpr int PPWA = (BM / 8 + NW - 1) / NW;   // 1 KiB LDS-DMA pieces of A per wave per stage
     constexpr int PPWB = (BNK / 8 + NW - 1) / NW;  // ... of B
     constexpr int PPW = PPWB;
@@ -166,13 +242,27 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     const int b = blockIdx.x;
     const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-    // pod-group major: PG pod tiles x every node tile per group
-    const int gsize = PG * n_mt;
-    const int g = v / gsize, r = v % gsize;
-    const int first_nt = g * PG;
-    const int pg = min(n_nt - first_nt, PG);
-    const int mt = r / pg;
-    const int nt = first_nt + r % pg;
+    int mt, nt;
+    if constexpr (GM > 0) {
+        // node-group major: GM node tiles x every pod tile, pod-minor
+        const int gsize = GM * n_nt;
+        const int g = v / gsize;
+        const int first_mt = g * GM;
+        const int gm = min(n_mt - first_mt, GM);
+        mt = first_mt + (v % gsize) % gm;
+        nt = (v % gsize) / gm;
+    } else {
+        // pod-group major (GM = -PG): PG pod tiles x every node tile, so an
+        // XCD keeps one pod group's traffic rows (PG x 2.5 MB at C3) hot in
+        // the memory-side cache while it sweeps the node tiles
+        constexpr int PG = GM < 0 ? -GM : 1;
+        const int gsize = PG * n_mt;
+        const int g = v / gsize, r = v % gsize;
+        const int first_nt = g * PG;
+        const int pg = min(n_nt - first_nt, PG);
+        mt = r / pg;
+        nt = first_nt + r % pg;
+    }
     const int cb = blockIdx.y;  // cluster of a batched launch
     if constexpr (FUSE) {
         fs.cap += (size_t)cb * 3 * fs.N;
@@ -206,6 +296,10 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
 
     const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
     const unsigned char *Bg = WA + (size_t)(p0 + nt * BNK) * Kb;
+    if constexpr (EPI == 3) {  // diagnostic: every block streams tile (0, 0): all L2 hits
+        Ag = Lt;
+        Bg = WA;
+    }
 
     // LDS-DMA staging: piece j of wave w fills rows (NW*j + w)*8 .. +8 of A
     // and of B (1 KiB each, lane-linear: lane l -> row + l/8, 16-byte chunk
@@ -214,9 +308,14 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // SOURCE address so fragment reads are bank-conflict free.
     const int srow_in = lane >> 3;
     const int sq = lane & 7;
-    // stage b of the double buffer: the A (latency) rows, then the B (traffic) rows
-    auto abuf = [&](int b) -> unsigned char * { return lds + b * STG; };
-    auto bbuf = [&](int b) -> unsigned char * { return lds + b * STG + BM * BKB; };
+    // buffer b of operand A / B (PIPE 0: A|B interleaved per stage; PIPE 1:
+    // A0 A1 B0 B1 B2)
+    auto abuf = [&](int b) -> unsigned char * {
+        return PIPE != 1 ? lds + b * STG : lds + b * TILE_BYTES;
+    };
+    auto bbuf = [&](int b) -> unsigned char * {
+        return PIPE != 1 ? lds + b * STG + TILE_BYTES : lds + (2 + b) * TILE_BYTES;
+    };
     // one 1 KiB LDS-DMA piece (8 rows x 128 B) of operand A / B: piece j of
     // wave w fills rows (NW*j + w)*8 .. +8
     auto pieceA = [&](int buf, int k0, int j) {
@@ -224,7 +323,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         const int r0 = (j * NW + w) * 8;
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
-        glds16(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
+        glds16<COST_AUX_A>(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
     };
     int bpod[PPW];  // RMAP: the WA rows of this lane's B pieces
     if constexpr (RMAP) {
@@ -238,7 +337,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
         const unsigned char *src = RMAP ? WA + (size_t)bpod[j] * Kb : Bg + (size_t)row * Kb;
-        glds16(src + k0 + c * 16, bbuf(buf) + r0 * BKB);
+        glds16<COST_AUX_B>(src + k0 + c * 16, bbuf(buf) + r0 * BKB);
     };
     // the wide tile stages A rows then B rows as one run of 80 pieces (the
     // B image follows the A image in LDS); piece pj of wave wu is 8 rows at
@@ -253,7 +352,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         if (pj >= (BM + BNK) / 8) return;
         const unsigned char *base = pj < BM / 8 ? Ag + (size_t)pj * 8 * Kb
                                                 : Bg + (size_t)(pj - BM / 8) * 8 * Kb;
-        glds16(base + k0 + loff, lds + buf * STG + pj * 8 * BKB);
+        glds16<0>(base + k0 + loff, lds + buf * STG + pj * 8 * BKB);
     };
     auto stageA = [&](int buf, int k0) {
         if constexpr (NWN == 6) {
@@ -355,7 +454,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // stay live across)
     u64 mwp[NI][2];
     auto load_mask = [&]() __attribute__((always_inline)) {
-        if constexpr (!FUSE) {
+        if constexpr (!FUSE && (EPI == 0 || EPI == 2 || EPI == 6)) {
 #pragma unroll
             for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
@@ -388,7 +487,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // (at 256 VGPRs the G = 8 rehearsal pass rose from 1.39 to 1.50 ms:
     // profiles/r03_bisect_g8.txt))
     constexpr bool OVF_ROUND2 = NWN == 6 || !FUSE;
-    if constexpr (OVF_ROUND2 && DT == NAS_DT_I8) {
+    if constexpr (OVF_ROUND2 && DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
         if (ov.ptr) {
             const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
             const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
@@ -417,8 +516,9 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             }
         }
     }
+    constexpr bool OVF_EARLY = COST_OVF_EARLY;
     auto seed_ovf = [&]() __attribute__((always_inline)) {
-        if constexpr (!OVF_ROUND2 && DT == NAS_DT_I8) {
+        if constexpr (!OVF_ROUND2 && DT == NAS_DT_I8 && (EPI == 0 || EPI == 2 || EPI == 6)) {
             if (ov.ptr) {
                 const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
                 const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
@@ -459,13 +559,18 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             }
         }
     };
-    if constexpr (NWN == 6) load_mask();
+    if constexpr (PIPE != 0 || OVF_EARLY) seed_ovf();
+    if constexpr (PIPE != 0 || OVF_EARLY || NWN == 6) load_mask();
 
     // fragments of k-substep kk+1 are read from LDS while the 8 MFMAs of kk
-    // run (register double buffer)
-    auto compute = [&](int buf) {
-        const unsigned char *As = abuf(buf);
-        const unsigned char *Bs = bbuf(buf);
+    // run (register double buffer; the just-in-time schedule hipcc picks on
+    // its own exposes the LDS latency every 4 MFMAs)
+    // compute one K-step from LDS; `piece(kk)` issues the next stage's LDS-DMA
+    // pieces that SCHED 5 spreads across the MFMA stream (their issue cost,
+    // 60-185 cycles each, otherwise stalls the wave at the top of the step)
+    auto compute = [&](int ab, int bbi, auto &&piece) {
+        const unsigned char *As = abuf(ab);
+        const unsigned char *Bs = bbuf(bbi);
         v4i a[2][4], bb[2][NI];
         auto read = [&](int kk, v4i (&ra)[4], v4i (&rb)[NI]) {
             const int c = kk * 2 + fh;
@@ -483,34 +588,300 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         read(0, a[0], bb[0]);
 #pragma unroll
         for (int kk = 0; kk < BKB / 32; ++kk) {
+            if constexpr (SCHED == 5) piece(kk);
             if (kk + 1 < BKB / 32) read(kk + 1, a[(kk + 1) & 1], bb[(kk + 1) & 1]);
+            if constexpr (SCHED == 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
                 for (int ni = 0; ni < NI; ++ni)
                     acc[mi][ni] = M::mma(a[kk & 1][mi], bb[kk & 1][ni], acc[mi][ni]);
+            if constexpr (SCHED == 2) __builtin_amdgcn_s_setprio(0);
+            if constexpr (SCHED == 1) {
+                // pin the interleave: MFMA, LDS read, MFMA, ... (6 reads of
+                // the next k-substep hidden under the 8 MFMAs of this one)
+                if (kk + 1 < BKB / 32) {
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                }
+            }
+            if constexpr (SCHED == 5) {
+                // MFMA, DMA piece, MFMA, LDS read, ... : 2 pieces + 6 reads in 8 MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (kk + 1 < BKB / 32) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (kk + 1 < BKB / 32) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    }
+                } else {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                }
+            }
+            if constexpr (SCHED == 3) __builtin_amdgcn_iglp_opt(0);
+            if constexpr (SCHED == 4) __builtin_amdgcn_iglp_opt(1);
         }
     };
+    auto nopiece = [](int) {};
 
-    // two-stage pipeline: stage t+1 streams in (LDS-DMA) while t is read
     const int nk = Kb / BKB;
-    stageA(0, 0);
-    stageB(0, 0);
-    seed_ovf();
-    if constexpr (NWN != 6) load_mask();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-        const int cur = t & 1;
-        if (t + 1 < nk) {
-            stageA(cur ^ 1, (t + 1) * BKB);
-            stageB(cur ^ 1, (t + 1) * BKB);
-        }
-        compute(cur);
+    if constexpr (EPI == 4 || EPI == 5) {
+        // diagnostic: stage once, then run the K loop on LDS only (4: with
+        // the per-step barrier, 5: without) -- the in-core ceiling
+        stageA(0, 0);
+        stageB(0, 0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int t = 0; t < nk; ++t) {
+            compute(0, 0, nopiece);
+            if constexpr (EPI == 4) {
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+            }
+        }
+    } else if constexpr (PIPE == 4) {
+        // Phased, staggered pipeline.  Each K-step is 4 phases (one 32-byte
+        // k-substep each); a phase is a LOAD segment (the next phase's 6
+        // fragment ds_reads + this wave's share of the next stage's LDS-DMA)
+        // and an MFMA segment (8 MFMAs at s_setprio 1), each closed by a raw
+        // s_barrier.  Waves 4-7 run one barrier behind waves 0-3, so on every
+        // SIMD one wave's MFMA segment overlaps its partner's load segment.
+        // Stage t+1 is issued in phases 0-1 of step t (4 pieces each), retired
+        // by a vmcnt(0) in phase 2's load segment and first read in phase 3's
+        // (a barrier apart, for both wave groups); its buffer's previous
+        // reads ended in phase 2 of step t-1.  No __syncthreads in the loop:
+        // its fence would drain the DMA.
+        v4i fa[2][4], fb[2][2];
+        auto readf = [&](int buf, int kk, v4i (&ra)[4], v4i (&rb)[2]) {
+            const unsigned char *As = abuf(buf);
+            const unsigned char *Bs = bbuf(buf);
+            const int c = kk * 2 + fh;
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int r = wm * 128 + mi * 32 + fr;
+                ra[mi] = *reinterpret_cast<const v4i *>(As + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+                const int r = wn * 64 + ni * 32 + fr;
+                rb[ni] = *reinterpret_cast<const v4i *>(Bs + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
+            }
+        };
+        auto mma8 = [&](const v4i (&ra)[4], const v4i (&rb)[2]) {
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+                for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = M::mma(ra[mi], rb[ni], acc[mi][ni]);
+            __builtin_amdgcn_s_setprio(0);
+        };
+        auto bar = [] {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // prologue: stage 0, fragments of (0, 0), then the stagger
+        stageA(0, 0);
+        stageB(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        readf(0, 0, fa[0], fb[0]);
+        if (wm == 1) bar();
+        // one K-step; MORE = a next stage exists (the last step is peeled, so
+        // the steady-state body is one basic block: hipcc's waitcnt pass then
+        // keeps the next phase's ds_reads in flight over the MFMA segment)
+        auto step = [&](int t, auto more_c) {
+            constexpr bool MORE = decltype(more_c)::value;
+            const int cur = t & 1;
+            const int kn = (t + 1) * BKB;
+            // phase 0 (fragment reads first, then the DMA pieces)
+            readf(cur, 1, fa[1], fb[1]);
+            if constexpr (MORE) {
+                pieceA(cur ^ 1, kn, 0); pieceA(cur ^ 1, kn, 1);
+                pieceB(cur ^ 1, kn, 0); pieceB(cur ^ 1, kn, 1);
+            }
+            bar();
+            mma8(fa[0], fb[0]);
+            bar();
+            // phase 1
+            readf(cur, 2, fa[0], fb[0]);
+            if constexpr (MORE) {
+                pieceA(cur ^ 1, kn, 2); pieceA(cur ^ 1, kn, 3);
+                pieceB(cur ^ 1, kn, 2); pieceB(cur ^ 1, kn, 3);
+            }
+            bar();
+            mma8(fa[1], fb[1]);
+            bar();
+            // phase 2: retire this wave's pieces of stage t+1 (vmcnt(0) only)
+            if constexpr (MORE) __builtin_amdgcn_s_waitcnt(0x0F70);
+            readf(cur, 3, fa[1], fb[1]);
+            bar();
+            mma8(fa[0], fb[0]);
+            bar();
+            // phase 3
+            if constexpr (MORE) readf(cur ^ 1, 0, fa[0], fb[0]);
+            bar();
+            mma8(fa[1], fb[1]);
+            bar();
+        };
+        for (int t = 0; t + 1 < nk; ++t) step(t, std::true_type{});
+        step(nk - 1, std::false_type{});
+        if (wm == 0) bar();  // re-align the barrier count of the two groups
+        __syncthreads();
+    } else if constexpr (PIPE >= 5) {
+        // two-stage pipeline + L2 touch of stage t + D: per step each wave
+        // issues its 8 pieces of stage t+1, then (if any) one touch, and
+        // waits vmcnt(1) -- the pieces and the previous step's touch have
+        // landed, this step's touch stays in flight across the raw barrier
+        constexpr int D = PIPE == 6 ? 3 : 2;
+        unsigned char *junk = lds + 2 * STAGE_BYTES;
+        // PIPE 5/6: threads 0..255 touch A row tid, 256..511 B row tid-256;
+        // PIPE 7: threads 0..255 touch B row tid, the other waves nothing
+        const bool toucher = PIPE != 7 || tid < 256;
+        const unsigned char *trow = (PIPE == 7 || tid >= 256) ? Bg + (size_t)(tid & 255) * Kb
+                                                              : Ag + (size_t)tid * Kb;
+        auto touch = [&](int k0) {
+            __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(trow + k0),
+                                             (void __attribute__((address_space(3))) *)junk, 4, 0, 0);
+        };
+        stageA(0, 0);
+        stageB(0, 0);
+        if (toucher && 1 < nk) touch(BKB);  // stage 1 (its own DMA comes at step 0)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int t = 0; t < nk; ++t) {
+            const int cur = t & 1;
+            if (t + 1 < nk) {
+                stageA(cur ^ 1, (t + 1) * BKB);
+                stageB(cur ^ 1, (t + 1) * BKB);
+            }
+            const bool tch = toucher && t + D < nk;
+            if (tch) touch((t + D) * BKB);
+            compute(cur, cur, nopiece);
+            if (tch) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        __syncthreads();
+    } else if constexpr (PIPE >= 2) {
+        // register-staged operands: step t+1's rows are loaded into VGPRs at
+        // the top of step t (latency hidden by its MFMAs) and written to the
+        // other LDS buffer (same swizzled image as the DMA path) at its end
+        v4i rb[4], ra[4];
+        auto gload = [&](const unsigned char *G, int k0, v4i (&r)[4]) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = (j * 8 + w) * 8 + srow_in;
+                r[j] = *reinterpret_cast<const v4i *>(G + (size_t)row * Kb + k0 + sq * 16);
+            }
+        };
+        auto lwrite = [&](unsigned char *L, const v4i (&r)[4]) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int row = (j * 8 + w) * 8 + srow_in;
+                const int c = sq ^ ((row >> 1) & 7);
+                *reinterpret_cast<v4i *>(L + row * BKB + c * 16) = r[j];
+            }
+        };
+        if constexpr (PIPE == 2) stageA(0, 0);
+        else gload(Ag, 0, ra);
+        gload(Bg, 0, rb);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (PIPE == 3) lwrite(abuf(0), ra);
+        lwrite(bbuf(0), rb);
+        __syncthreads();
+        for (int t = 0; t < nk; ++t) {
+            const int cur = t & 1;
+            const bool more = t + 1 < nk;
+            if (more) {
+                if constexpr (PIPE == 2) stageA(cur ^ 1, (t + 1) * BKB);
+                else gload(Ag, (t + 1) * BKB, ra);
+                gload(Bg, (t + 1) * BKB, rb);
+            }
+            compute(cur, cur, nopiece);
+            if (more) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if constexpr (PIPE == 3) lwrite(abuf(cur ^ 1), ra);
+                lwrite(bbuf(cur ^ 1), rb);
+            }
+            __syncthreads();
+        }
+    } else if constexpr (PIPE == 0) {
+        // two-stage pipeline: stage t+1 streams in (LDS-DMA) while t is read
+        stageA(0, 0);
+        stageB(0, 0);
+        if constexpr (!OVF_EARLY) seed_ovf();
+        if constexpr (!OVF_EARLY && NWN != 6) load_mask();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        for (int t = 0; t < nk; ++t) {
+            const int cur = t & 1;
+            const bool more = t + 1 < nk;
+            if constexpr (SCHED == 5) {
+                compute(cur, cur, [&](int kk) {
+                    if (more) {
+                        pieceA(cur ^ 1, (t + 1) * BKB, kk);
+                        pieceB(cur ^ 1, (t + 1) * BKB, kk);
+                    }
+                });
+            } else {
+                if (more) {
+                    stageA(cur ^ 1, (t + 1) * BKB);
+                    stageB(cur ^ 1, (t + 1) * BKB);
+                }
+                compute(cur, cur, nopiece);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+    } else {
+        // A one stage ahead, B two stages ahead.  Issue order per step is
+        // A(t+1) then B(t+2), so vmcnt(4) (= B's 4 pieces per wave) leaves
+        // exactly B(t+2) in flight across the barrier; a raw s_barrier (no
+        // __syncthreads, whose fence would drain it) ends the step.
+        stageA(0, 0);
+        stageB(0, 0);
+        if (nk > 1) stageB(1, BKB);
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        int b3 = 0;  // t % 3
+        for (int t = 0; t < nk; ++t) {
+            if (t + 1 < nk) stageA((t + 1) & 1, (t + 1) * BKB);
+            if (t + 2 < nk) stageB(b3 == 0 ? 2 : b3 - 1, (t + 2) * BKB);  // (t+2) % 3
+            compute(t & 1, b3, nopiece);
+            if (t + 2 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            b3 = b3 == 2 ? 0 : b3 + 1;
+        }
         __syncthreads();
     }
 
+    if constexpr (EPI == 1 || (EPI >= 3 && EPI <= 5)) {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                asm volatile("" ::"v"(acc[mi][ni]));
+#endif
+            }
+        return;
+    }
     if constexpr (NWN == 6) {
         // the lane index afresh (volatile: not CSE'd with the prologue's), so
         // the old one dies in the loop
@@ -565,7 +936,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             kmax = M::okey(smax);
         }
         u64 k4[4];
-        if (__all(kmax - kmin < (1u << 26) - 1u)) {
+        if (EPI == 0 && __all(kmax - kmin < (1u << 26) - 1u)) {
             // packed path (every lane's keys span < 2^26 - 1): one u32 per
             // value, (key - kmin) << 6 | i with i = mi*16 + reg increasing in
             // node order, so u32 order = (cost, node) order; a non-fitting
@@ -633,6 +1004,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         } else {
             Top4 t4;
             t4.init();
+            unsigned best1 = 0xffffffffu, bnode1 = 0xffffffffu;
 #pragma unroll
             for (int mi2 = 0; mi2 < 2; ++mi2) {
 #pragma unroll
@@ -646,10 +1018,17 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                         // not fitting -> cost all-ones, never inserted (branch-free)
                         const unsigned key = DT == NAS_DT_I8 ? M::okey(acc[mi][ni][reg]) : u[mi][reg];
                         const unsigned x = key | ((((bits >> row) & 1u) ^ 1u) * 0xffffffffu);
-                        t4.insert(x, node0 + row);
+                        if constexpr (EPI == 2) {
+                            const bool b = x < best1;
+                            best1 = b ? x : best1;
+                            bnode1 = b ? node0 + row : bnode1;
+                        } else {
+                            t4.insert(x, node0 + row);
+                        }
                     }
                 }
             }
+            if constexpr (EPI == 2) t4.c[0] = best1, t4.n[0] = bnode1;
 #pragma unroll
             for (int j = 0; j < 4; ++j) k4[j] = t4.c[j] == 0xffffffffu ? KEY_INVALID : t4.key(j);
         }
@@ -764,14 +1143,31 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
     dst_bound[p] = umin64(bound, a[7]);
 }
 
-template <int DT, bool RMAP, int NWN = 4, bool FUSE = (NWN == 6)>
+#ifdef NAS_DIAG_VARIANTS
+#define NAS_INST(E, S, PP, G)                                                                      \
+    template __global__ void k_cost_topk<NAS_DT_I8, E, S, PP, G>(                                  \
+        const unsigned char *, const unsigned char *, int, int, int, int, int, const u64 *, u64 *,  \
+        u64 *, int, const int *, int, const int *, Ovf, const int *, FitSrc);
+NAS_INST(0, 0, 0, 4) NAS_INST(1, 0, 0, 4) NAS_INST(0, 5, 0, 4) NAS_INST(1, 5, 0, 4)
+NAS_INST(3, 5, 0, 4) NAS_INST(0, 1, 0, 4) NAS_INST(0, 5, 0, 8) NAS_INST(4, 0, 0, 4)
+NAS_INST(0, 1, 2, 4) NAS_INST(0, 1, 3, 4) NAS_INST(0, 0, 2, 4) NAS_INST(0, 0, 3, 4)
+NAS_INST(1, 1, 2, 4) NAS_INST(1, 1, 3, 4)
+NAS_INST(0, 0, 4, 4) NAS_INST(1, 0, 4, 4) NAS_INST(0, 0, 4, 8) NAS_INST(0, 0, 4, 2)
+NAS_INST(0, 0, 0, -2) NAS_INST(0, 0, 0, -4) NAS_INST(0, 0, 0, -8) NAS_INST(0, 0, 0, 8)
+NAS_INST(0, 0, 0, 2) NAS_INST(0, 0, 0, 16)
+#undef NAS_INST
+
+#endif
+
+template <int DT, bool RMAP, int NWN = cost_nwn<DT>(), bool FUSE = (NWN == 6)>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,
                          int p0, int np, const uint64_t *mask, uint64_t *partial,
                          uint64_t *pbound, int node_base, const Dyn *dyn, int batch,
                          const Ovf &ov, const int32_t *rowmap, const FitSrc &fs = FitSrc{}) {
-    constexpr int BNK = NWN * 64;
-    const void *fn = reinterpret_cast<const void *>(&k_cost_topk<DT, RMAP, NWN, FUSE>);
-    constexpr int lds = 2 * (BM + BNK) * BKB;
+    constexpr int BNK = NWN * (NWN == 2 ? 128 : 64);
+    const void *fn = reinterpret_cast<const void *>(
+        &k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, NWN == 6 ? COST_GM_WIDE : COST_GM, RMAP, NWN, FUSE>);
+    const int lds = NWN == 6 ? 2 * (BM + BNK) * BKB : lds_bytes<COST_PIPE>();
     static std::atomic<unsigned long long> attr_set{0};
     hipError_t e = set_lds_once(fn, lds, attr_set);
     if (e != hipSuccess) return e;
@@ -793,14 +1189,17 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const int *dhp = dyn ? dyn->hi_ptr : nullptr;
     // the wide tile's launch end rides in dyn_hi (unused without a window)
     const int dhi = NWN == 6 ? p0 + np : dh;
-    k_cost_topk<DT, RMAP, NWN, FUSE><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
+    k_cost_topk<DT, 0, COST_SCHED, COST_PIPE, NWN == 6 ? COST_GM_WIDE : COST_GM, RMAP, NWN, FUSE><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
         lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dhi, dhp, ov, rowmap, fs);
     return hipGetLastError();
 }
 
 }  // namespace
 
-int cost_tile_pods(int) { return WIDE_PODS; }
+int cost_tile_pods(int dtype) {
+    const bool wide = dtype == NAS_DT_I8 ? cost_wide<NAS_DT_I8>() : cost_wide<NAS_DT_BF16>();
+    return wide ? 384 : BN;
+}
 
 // Kp: padded contraction length in ELEMENTS; np: pods, multiple of BN,
 // p0 + np <= Pp; Mp multiple of BM.
@@ -816,10 +1215,10 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
 #define NAS_COST_DISPATCH(DTV, KB, OVV)                                                            \
     (rowmap ? launch_cost_t<DTV, true>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound,     \
                                        node_base, dyn, batch, OVV, rowmap)                        \
-     : (!dyn && wide)                                                                             \
+     : (!dyn && wide && cost_wide<DTV>())                                                                 \
             ? launch_cost_t<DTV, false, 6>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound, \
                                            node_base, dyn, batch, OVV, nullptr, *fit)             \
-     : fit ? launch_cost_t<DTV, false, 4, true>(st, Lt, WA, Mp, KB, Pp, p0, np,     \
+     : fit ? launch_cost_t<DTV, false, cost_nwn<DTV>(), true>(st, Lt, WA, Mp, KB, Pp, p0, np,     \
                                                              mask, partial, pbound, node_base,    \
                                                              dyn, batch, OVV, nullptr, *fit)      \
             : launch_cost_t<DTV, false>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound,    \

@@ -3,7 +3,7 @@
 // LDS-DMA cache policy per operand).  Diagnostics only; not part of libnas.so.
 // Build one binary per knob setting (tools/mb_aux.sh) and run them alternately
 // on one box: prints "<tag> <variant> <ms>" per launch.
-#include "../k_cost.hip"
+#include "k_cost_diag.hip"
 
 #include <cstdio>
 #include <cstdlib>

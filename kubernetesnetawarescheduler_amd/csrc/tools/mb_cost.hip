@@ -2,7 +2,7 @@
 // (diagnostics only; not part of libnas.so).  Times each variant with HIP
 // events over back-to-back launches on random operands, interleaved.
 #define NAS_DIAG_VARIANTS
-#include "../k_cost.hip"
+#include "k_cost_diag.hip"
 #include "k_cost_experiments.hip"
 
 #include <cstdio>
