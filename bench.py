@@ -358,7 +358,9 @@ def bench_fit_kernel(args, d, eng, reps=10):
             "frac": algo / (fit_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "launch_ms": fit_ms,
             "launch_ms_min": min(ms), "launches": reps, "bytes_per_launch": algo,
             "note": "mask write P*ceil(N/64)*8 B + capacities and requests 12*(N+P) B per launch; "
-                    "HIP events around the one launch"}
+                    "HIP events around the one launch.  The standalone filter only: in the "
+                    "world-1 placement pass the wide cost kernel decides the fit itself after "
+                    "its main loop (fused fit), so no k_fit launch runs there"}
 
 
 def vendor_gemm_reference(args, d, reps=5):
@@ -1021,8 +1023,10 @@ def main():
                            "frac": achieved / peak,
                            "traffic": traffic.get("k_cost_topk", {}).get("bytes"),
                            "traffic_unit": "B/launch",
-                           "traffic_note": ("HBM-side bytes of the largest k_cost_topk dispatch, "
-                                            "rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE in this run"
+                           "traffic_note": ("beyond-L2 bytes of the largest k_cost_topk dispatch "
+                                            "(rocprofv3 FETCH_SIZE x 2, which counts the L2's "
+                                            "memory-side requests incl. Infinity Cache hits, "
+                                            "+ WRITE_SIZE) in this run"
                                             if traffic else traffic_why),
                            "launch_ms": cost_ms, "launches": len(samples),
                            "launch_ms_min": min(samples), "ops_per_launch": ops,

@@ -1241,12 +1241,15 @@ float decode_cost(uint32_t raw, int dtype) {
 void destroy_comms(nas_ctx *ctx) {
     // non-blocking communicators: finalize (flush, in RCCL's async job), poll
     // it to completion, then destroy; a finalize that fails or does not
-    // finish within 10 s is aborted instead (local, no peer handshake)
+    // finish within 10 s -- one deadline for all three, so peers that already
+    // exited cost 10 s, not 30 -- is aborted instead (local, no peer
+    // handshake); a poisoned context (a collective missed its deadline)
+    // aborts at once
+    const auto limit = std::chrono::steady_clock::now() + std::chrono::seconds(10);
     for (ncclComm **c : {&ctx->comm, &ctx->comm2, &ctx->comm_c}) {
         if (!*c) continue;
         auto comm = reinterpret_cast<ncclComm_t>(*c);
-        ncclResult_t r = ncclCommFinalize(comm);
-        const auto limit = std::chrono::steady_clock::now() + std::chrono::seconds(10);
+        ncclResult_t r = ctx->poisoned ? ncclInvalidUsage : ncclCommFinalize(comm);
         while (r == ncclInProgress && std::chrono::steady_clock::now() < limit) {
             ncclResult_t a = ncclInProgress;
             const ncclResult_t q = ncclCommGetAsyncError(comm, &a);
@@ -1278,6 +1281,40 @@ void destroy_comms(nas_ctx *ctx) {
     }
 }
 
+}  // namespace
+
+// state of one nas_comm_init, shared with its helper thread (see there)
+struct nas::CommInit {
+    enum { ROOT = 3 };  // handle index: 0..2 the children, 3 the root
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    unsigned claimed = 0;  // bit i: handle i is the main thread's to abort (or already aborted)
+    ncclComm_t root = nullptr;                         // written by RCCL from the helper
+    ncclComm_t kids[3] = {nullptr, nullptr, nullptr};  // likewise
+    ncclResult_t r = ncclSuccess;
+    std::string what;
+};
+
+namespace {
+// join the parked helpers of earlier abandoned inits: the finished ones
+// (wait = false), or all of them (nas_destroy)
+void reap_comm_helpers(nas_ctx *ctx, bool wait) {
+    for (size_t i = 0; i < ctx->comm_helpers.size();) {
+        bool done = wait;
+        if (!wait) {
+            std::lock_guard<std::mutex> g(ctx->comm_helper_state[i]->mu);
+            done = ctx->comm_helper_state[i]->done;
+        }
+        if (!done) {
+            ++i;
+            continue;
+        }
+        ctx->comm_helpers[i].join();
+        ctx->comm_helpers.erase(ctx->comm_helpers.begin() + i);
+        ctx->comm_helper_state.erase(ctx->comm_helper_state.begin() + i);
+    }
+}
 }  // namespace
 
 extern "C" {
@@ -1334,6 +1371,7 @@ void nas_destroy(nas_ctx *ctx) {
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
     if (ctx->ref_stage.p) (void)hipHostFree(ctx->ref_stage.p);
     destroy_comms(ctx);
+    reap_comm_helpers(ctx, true);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->stream2);
@@ -2459,46 +2497,64 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     // every rank), each warmed up by one small all-gather so its connections
     // exist before the first pass (the pass's collectives then enqueue at
     // once; nccl_enqueued polls the rare ncclInProgress).  This thread waits
-    // under NAS_OPT_COMM_TIMEOUT_MS; on expiry it aborts every published
-    // communicator, which ends the helper's bootstrap wait (measured: the
-    // helper returns ~2.5 s after the abort), joins the helper and returns
-    // NAS_ERR_COMM -- no thread of this call outlives it, so a host may retry.
-    struct Init {
-        std::mutex mu;
-        std::condition_variable cv;
-        bool done = false, abandoned = false, aborted = false;
-        ncclComm_t root = nullptr;                       // written by RCCL from the helper
-        ncclComm_t kids[3] = {nullptr, nullptr, nullptr};  // likewise
-        ncclResult_t r = ncclSuccess;
-        std::string what;
-    };
-    auto st = std::make_shared<Init>();
+    // under NAS_OPT_COMM_TIMEOUT_MS; on expiry it CLAIMS every published
+    // handle under the state's mutex and aborts it, which ends the helper's
+    // bootstrap wait (measured: the helper returns ~2.5 s after the abort).
+    // Handle ownership: the helper touches a handle only under the mutex and
+    // only while it is unclaimed (except inside the init call that creates
+    // it), so no RCCL call of the helper races the main thread's abort; a
+    // handle that appears after the claim is aborted by the helper itself.
+    // A helper still inside RCCL 30 s after the aborts is parked in the
+    // context (joined by the next nas_comm_init once done, or by
+    // nas_destroy): no thread of this call is ever detached.
+    reap_comm_helpers(ctx, false);
+    auto st = std::make_shared<nas::CommInit>();
     const int dev = ctx->device;
+    using CI = nas::CommInit;
     std::thread helper([st, dev, uid, rank, world]() mutable {
+        auto load = [](ncclComm_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); };
+        auto slot = [&](int i) -> ncclComm_t * { return i == CI::ROOT ? &st->root : &st->kids[i]; };
+        // run f(handle i) under the mutex unless the init was abandoned or
+        // the main thread claimed the handle
+        auto guarded = [&](int i, auto &&f) -> ncclResult_t {
+            std::lock_guard<std::mutex> g(st->mu);
+            if (st->abandoned || (st->claimed >> i & 1u)) return ncclInvalidUsage;
+            return f(load(slot(i)));
+        };
+        // poll handle i until its pending work is done
+        auto settle = [&](int i) -> ncclResult_t {
+            for (;;) {
+                ncclResult_t a = ncclInProgress;
+                const ncclResult_t q = guarded(i, [&](ncclComm_t c) { return ncclCommGetAsyncError(c, &a); });
+                if (q != ncclSuccess) return q;
+                if (a != ncclInProgress) return a;
+                std::this_thread::sleep_for(std::chrono::microseconds(200));
+            }
+        };
+        // an init call returned: if the call was abandoned meanwhile, the
+        // handle it published after the main thread's claim is ours to abort
+        auto after_init = [&](int i, ncclResult_t r) -> ncclResult_t {
+            std::lock_guard<std::mutex> g(st->mu);
+            if (!st->abandoned) return r;
+            ncclComm_t c = load(slot(i));
+            if (c && !(st->claimed >> i & 1u)) {
+                st->claimed |= 1u << i;
+                (void)ncclCommAbort(c);
+            }
+            return ncclInvalidUsage;
+        };
         auto abandoned = [&] {
             std::lock_guard<std::mutex> g(st->mu);
             return st->abandoned;
         };
-        // poll a communicator of this call until its pending work is done
-        auto settle = [&](ncclComm_t c) -> ncclResult_t {
-            for (;;) {
-                ncclResult_t a = ncclInProgress;
-                const ncclResult_t q = ncclCommGetAsyncError(c, &a);
-                if (q != ncclSuccess) return q;
-                if (a != ncclInProgress) return a;
-                if (abandoned()) return ncclInvalidUsage;
-                std::this_thread::sleep_for(std::chrono::microseconds(200));
-            }
-        };
-        auto load = [](ncclComm_t *p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); };
         ncclResult_t r = hipSetDevice(dev) == hipSuccess ? ncclSuccess : ncclUnhandledCudaError;
         std::string what = "hipSetDevice";
         if (r == ncclSuccess) {
             what = "ncclCommInitRankConfig";
             ncclConfig_t rc = NCCL_CONFIG_INITIALIZER;
             rc.blocking = 0;
-            r = ncclCommInitRankConfig(&st->root, world, uid, rank, &rc);
-            if (r == ncclInProgress && load(&st->root)) r = settle(load(&st->root));
+            r = after_init(CI::ROOT, ncclCommInitRankConfig(&st->root, world, uid, rank, &rc));
+            if (r == ncclInProgress && load(&st->root)) r = settle(CI::ROOT);
             if (r == ncclSuccess && !load(&st->root)) r = ncclInternalError;
         }
         hipStream_t s = nullptr;
@@ -2541,9 +2597,10 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
                 hipMemcpyAsync(buf, kid_ids, ids_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
                 r = ncclUnhandledCudaError;
             if (r == ncclSuccess) {
-                ncclComm_t root = load(&st->root);
-                r = ncclBroadcast(buf, buf, ids_bytes, ncclUint8, 0, root, s);
-                if (r == ncclInProgress) r = settle(root);
+                r = guarded(CI::ROOT, [&](ncclComm_t root) {
+                    return ncclBroadcast(buf, buf, ids_bytes, ncclUint8, 0, root, s);
+                });
+                if (r == ncclInProgress) r = settle(CI::ROOT);
                 inflight = r == ncclSuccess;
             }
             if (r == ncclSuccess &&
@@ -2556,8 +2613,8 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
             what = "ncclCommInitRankConfig (child)";
             ncclConfig_t kc = NCCL_CONFIG_INITIALIZER;
             kc.blocking = NAS_COMM_CHILD_BLOCKING;
-            r = ncclCommInitRankConfig(&st->kids[i], world, kid_ids[i], rank, &kc);
-            if (r == ncclInProgress && load(&st->kids[i])) r = settle(load(&st->kids[i]));
+            r = after_init(i, ncclCommInitRankConfig(&st->kids[i], world, kid_ids[i], rank, &kc));
+            if (r == ncclInProgress && load(&st->kids[i])) r = settle(i);
             if (r == ncclSuccess && !load(&st->kids[i])) r = ncclInternalError;
         }
         if (r == ncclSuccess) {
@@ -2566,9 +2623,8 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
             what = "warm-up all-gather";
             char *w = static_cast<char *>(buf) + ids_bytes;
             for (int i = 0; i < 3 && r == ncclSuccess; ++i) {
-                ncclComm_t k = load(&st->kids[i]);
-                r = ncclAllGather(w, w + 8, 1, ncclUint64, k, s);
-                if (r == ncclInProgress) r = settle(k);
+                r = guarded(i, [&](ncclComm_t k) { return ncclAllGather(w, w + 8, 1, ncclUint64, k, s); });
+                if (r == ncclInProgress) r = settle(i);
                 inflight = inflight || r == ncclSuccess;
             }
             if (r == ncclSuccess) r = drain();
@@ -2591,12 +2647,14 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
         }
         std::lock_guard<std::mutex> g(st->mu);
         if (r == ncclSuccess && st->abandoned) r = ncclInvalidUsage;
-        if (r != ncclSuccess && !st->aborted) {  // abort: local, no peer handshake
-            for (ncclComm_t &k : st->kids)
-                if (k) (void)ncclCommAbort(k);
-            if (st->root) (void)ncclCommAbort(st->root);
-        }
         if (r != ncclSuccess) {
+            // abort (local, no peer handshake) every handle the main thread
+            // did not claim; the claimed ones are its to abort
+            for (int i = 0; i < 4; ++i) {
+                ncclComm_t c = load(slot(i));
+                if (c && !(st->claimed >> i & 1u)) (void)ncclCommAbort(c);
+                st->claimed |= 1u << i;
+            }
             for (ncclComm_t &k : st->kids) k = nullptr;
             st->root = nullptr;
         }
@@ -2612,20 +2670,25 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
         expired = !st->cv.wait_for(lk, limit, [&] { return st->done; });
         if (expired) {
             // the root's handle appears ~1 s into the init: wait for it (or for
-            // the helper to finish) a bounded while, then abort what exists
+            // the helper to finish) a bounded while, then claim and abort what
+            // exists -- claimed under the mutex, aborted outside it (the
+            // helper may need the mutex to leave the RCCL call the abort ends)
             st->abandoned = true;
             const auto grace = std::chrono::steady_clock::now() + std::chrono::seconds(30);
             while (!st->done && !__atomic_load_n(&st->root, __ATOMIC_ACQUIRE) &&
                    std::chrono::steady_clock::now() < grace)
                 st->cv.wait_for(lk, std::chrono::milliseconds(20));
             if (!st->done) {
-                ncclComm_t hs[4];
-                for (int i = 0; i < 3; ++i) hs[i] = __atomic_load_n(&st->kids[i], __ATOMIC_ACQUIRE);
-                hs[3] = __atomic_load_n(&st->root, __ATOMIC_ACQUIRE);
-                st->aborted = true;
+                std::vector<ncclComm_t> mine;
+                for (int i = 0; i < 4; ++i) {
+                    ncclComm_t c = __atomic_load_n(i == CI::ROOT ? &st->root : &st->kids[i], __ATOMIC_ACQUIRE);
+                    if (c && !(st->claimed >> i & 1u)) {
+                        st->claimed |= 1u << i;
+                        mine.push_back(c);
+                    }
+                }
                 lk.unlock();
-                for (ncclComm_t h : hs)  // ends the helper's waits inside RCCL
-                    if (h) (void)ncclCommAbort(h);
+                for (ncclComm_t h : mine) (void)ncclCommAbort(h);  // ends the helper's waits
                 lk.lock();
             }
             st->cv.wait_until(lk, grace, [&] { return st->done; });
@@ -2635,15 +2698,21 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     }
     const bool finished = st->done;
     lk.unlock();
-    if (finished) helper.join();
-    else helper.detach();  // (the aborts did not release it within 30 s)
+    if (finished) {
+        helper.join();
+    } else {
+        // (the aborts did not release it within 30 s) parked, joined later
+        ctx->comm_helpers.push_back(std::move(helper));
+        ctx->comm_helper_state.push_back(st);
+    }
     if (expired)
         return nas::fail(ctx, NAS_ERR_COMM,
                          "nas_comm_init: the communicators did not complete within " +
                              std::to_string(ctx->opt_comm_timeout_ms) +
                              " ms (NAS_OPT_COMM_TIMEOUT_MS): a rank did not join; "
                              "communicators aborted" +
-                             (finished ? "" : " (helper thread still blocked in RCCL)"));
+                             (finished ? "" : " (the helper thread is still inside RCCL: parked in the "
+                                              "context, joined by nas_destroy)"));
     if (st->r != ncclSuccess)
         return nas::fail(ctx, NAS_ERR_COMM, st->what + ": " + ncclGetErrorString(st->r));
     ctx->rank = rank;

@@ -9,6 +9,7 @@
 #include <atomic>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/nas.h"
@@ -85,6 +86,7 @@ struct LocalSrcs {
     const void *p[LOCAL_MAX_WORLD];
 };
 struct LocalGroup;  // nas_api.hip
+struct CommInit;    // nas_api.hip: state shared with a nas_comm_init helper thread
 
 }  // namespace nas
 
@@ -191,6 +193,10 @@ struct nas_ctx {
     uint32_t lg_round[3] = {0, 0, 0};
     hipEvent_t lg_ev[3][2][2] = {};
     uint64_t lg_peers = 0;
+    // nas_comm_init helper threads still inside RCCL after an abandoned init
+    // (joined by the next nas_comm_init once finished, or by nas_destroy)
+    std::vector<std::thread> comm_helpers;
+    std::vector<std::shared_ptr<nas::CommInit>> comm_helper_state;
     // options (nas_set_option)
     bool opt_stage_timings = true;
     int64_t opt_comm_timeout_ms = 120000;
