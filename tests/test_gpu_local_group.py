@@ -77,8 +77,9 @@ def test_local_group_place_equals_oracle(G, P, N, crowd):
             assert (cap == wfree).all(), (G, r)
             if crowd:
                 assert t["rescore_rounds"] > 0, (G, r, t)
-    # every rank walked the same commit
-    assert len({p[0][3]["commit_rounds"] for p in res}) == 1
+    # (commit_rounds may differ between ranks and runs: which reservation of a
+    # window fails first depends on the order its atomics land -- the
+    # placements do not, as checked above)
 
 
 def test_local_group_bf16_equals_oracle():
