@@ -1102,6 +1102,9 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
 #ifndef CHUNK_FIRST_HALF
 #define CHUNK_FIRST_HALF 0
 #endif
+#ifndef TAIL_SDMA
+#define TAIL_SDMA 1
+#endif
 #ifndef CHUNK_MIN_TAIL
 #define CHUNK_MIN_TAIL 0  // 256-pod units: a stream's last chunk at least this long
 #endif
@@ -2179,10 +2182,22 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         }
         OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx)));
         hipEvent_t c0 = tm.fine(cs);
+        // the tail chunk's results go to the host by DMA copies behind its
+        // commit (the scoring is over, nothing delays them), not by the
+        // commit workgroup's own stores over the host link
+        const bool sdma = tail && TAIL_SDMA;
         HIPCK(nas::launch_commit(cs, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
-                                 1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr));
+                                 1, pub, zrow_ptr(ctx), sdma ? nullptr : stage,
+                                 (want_raw && !sdma) ? stage + P : nullptr));
+        if (sdma) {
+            HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo, (size_t)(hi - lo) * 4,
+                                 hipMemcpyDeviceToHost, cs));
+            if (want_raw)
+                HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
+                                     (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, cs));
+        }
         tm.span(T_COMMIT, c0, tm.fine(cs));
         // the commit wrote this chunk's results into the pinned stage as it
         // ended, and the host unpacks them while later chunks still run

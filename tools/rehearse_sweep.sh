@@ -10,6 +10,6 @@ B="--only place --no-cpu-baseline --no-pmc --no-configs --no-reference-mode"
     -- python3 "$ROOT/bench.py" $B --rehearse-world 8 --steps 5 --warmup 2 > "$OUT/g8.json" 2>&1 ) || { echo "trace failed"; exit 1; }
 python3 tools/pass_timeline.py "$OUT/tr8" > "$OUT/g8_timeline.txt"
 for G in 1 2 4 8; do
-  timeout -k 10 120 python3 bench.py $B --rehearse-world $G --steps 30 --warmup 3 > "$OUT/reh$G.json" 2>&1 || exit 1
+  timeout -k 10 120 python3 bench.py $B --rehearse-world $G --steps 30 --warmup 3 > "$OUT/reh$G.json" 2> "$OUT/reh$G.err" || exit 1
   python3 -c "import json; d=json.load(open('$OUT/reh$G.json')); print($G, round(d['ms_per_step'],3), round(d['roofline']['launch_ms'],3))"
 done
