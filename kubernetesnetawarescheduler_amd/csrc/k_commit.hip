@@ -254,13 +254,22 @@ __device__ __forceinline__ void to_stage(const int *out_node, const unsigned *ou
     }
 }
 
+// the status words (after this walk's updates, by the thread that made them)
+// into the host's pinned status area: the pass's last commit, so the host's
+// wait for it brings the status with the results
+__device__ __forceinline__ void status_to_stage(const int *halt, int *stage_status) {
+    if (!stage_status) return;
+#pragma unroll
+    for (int j = 0; j < COMMIT_STATUS_WORDS; ++j) stage_status[j] = halt[j];
+}
+
 template <bool LDS_CAP>
 __global__ void __launch_bounds__(THREADS)
 k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
          const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
          int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
          int *__restrict__ halt, int *__restrict__ pub, const unsigned char *__restrict__ zrow,
-         int *__restrict__ stage_node, unsigned *__restrict__ stage_cost) {
+         int *__restrict__ stage_node, unsigned *__restrict__ stage_cost, int *__restrict__ stage_status) {
     // one workgroup per cluster of a batched launch
     const int cb = blockIdx.x;
     cand_key += (size_t)cb * Pp * KC;
@@ -283,12 +292,11 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     // (nothing to do unless a walk halted), clearing the halt word
     const int h = __hip_atomic_load(halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool resume = p_begin < 0;
-    if (resume) {
-        if (h < 0) return;
-        p_begin = h;
-    } else if (h >= 0) {
+    if (resume ? h < 0 : h >= 0) {  // nothing to walk (the status still goes out)
+        if (threadIdx.x == 0) status_to_stage(halt, stage_status);
         return;
     }
+    if (resume) p_begin = h;
     if (LDS_CAP) cap_to_lds(cap_g, capl, 3 * N, tid >> 6, THREADS / 64);
     int *cap = LDS_CAP ? capl : cap_g;
     if (tid == 0) first_bad[0] = first_bad[1] = first_bad[2] = NO_POD;
@@ -437,6 +445,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     if (tid == 0) {
         if (stop < p_end) *halt = stop;
         halt[2] += round;  // rounds walked, reported in nas_timings
+        status_to_stage(halt, stage_status);
     }
     __syncthreads();
     to_stage(out_node, out_cost, stage_node ? stage_node + (size_t)cb * p_end : nullptr,
@@ -505,7 +514,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
            const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
            int N, int *__restrict__ out_node, unsigned *__restrict__ out_cost,
            int *__restrict__ halt, int *__restrict__ pub, const unsigned char *__restrict__ zrow,
-           int *__restrict__ stage_node, unsigned *__restrict__ stage_cost) {
+           int *__restrict__ stage_node, unsigned *__restrict__ stage_cost, int *__restrict__ stage_status) {
     const int cb = blockIdx.x;
     cand_key += (size_t)cb * Pp * KC;
     cand_bound += (size_t)cb * Pp;
@@ -521,12 +530,11 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     const int lane = threadIdx.x;
     const int h = __hip_atomic_load(halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool resume = p_begin < 0;
-    if (resume) {
-        if (h < 0) return;
-        p_begin = h;
-    } else if (h >= 0) {
+    if (resume ? h < 0 : h >= 0) {  // nothing to walk (the status still goes out)
+        if (threadIdx.x == 0) status_to_stage(halt, stage_status);
         return;
     }
+    if (resume) p_begin = h;
     if (LDS_CAP) cap_to_lds(cap_g, capl, 3 * N, 0, 1);
     int *cap = LDS_CAP ? capl : cap_g;
     struct Pod {
@@ -716,6 +724,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     if (lane == 0) {
         if (stop < p_end) *halt = stop;
         halt[2] += round;
+        status_to_stage(halt, stage_status);
     }
     __syncthreads();  // (one wave: every lane's placements written)
     to_stage(out_node, out_cost, stage_node ? stage_node + (size_t)cb * p_end : nullptr,
@@ -732,10 +741,11 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost, int32_t *halt, int batch,
                          int32_t *pub, const uint8_t *zrow, int32_t *stage_node,
-                         int32_t *stage_cost) {
+                         int32_t *stage_cost, int32_t *stage_status) {
     if (p_begin >= 0 && p_end <= p_begin) return hipSuccess;
     // a batch stages whole clusters, [cluster][p_end] rows from pod 0
     if (stage_node && (p_begin < 0 || (batch != 1 && p_begin != 0))) return hipErrorInvalidValue;
+    if (stage_status && batch != 1) return hipErrorInvalidValue;
     auto *sc = reinterpret_cast<unsigned *>(stage_cost);
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
@@ -748,10 +758,10 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
                                         LDS_DYN_MAX, attr);
             if (e != hipSuccess) return e;
             k_commit_w<true><<<batch, 64, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
-                                                     out_node, oc, halt, nullptr, zrow, stage_node, sc);
+                                                     out_node, oc, halt, nullptr, zrow, stage_node, sc, stage_status);
         } else {
             k_commit_w<false><<<batch, 64, PF_BYTES, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
-                                                           out_node, oc, halt, pub, zrow, stage_node, sc);
+                                                           out_node, oc, halt, pub, zrow, stage_node, sc, stage_status);
         }
         return hipGetLastError();
     }
@@ -761,10 +771,10 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
         hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit<true>), LDS_DYN_MAX, attr);
         if (e != hipSuccess) return e;
         k_commit<true><<<batch, THREADS, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
-                                                oc, halt, nullptr, zrow, stage_node, sc);
+                                                oc, halt, nullptr, zrow, stage_node, sc, stage_status);
     } else {
         k_commit<false><<<batch, THREADS, 0, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N, out_node,
-                                               oc, halt, pub, zrow, stage_node, sc);
+                                               oc, halt, pub, zrow, stage_node, sc, stage_status);
     }
     return hipGetLastError();
 }

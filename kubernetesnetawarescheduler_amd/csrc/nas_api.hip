@@ -1102,8 +1102,9 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
 #ifndef CHUNK_FIRST_HALF
 #define CHUNK_FIRST_HALF 0
 #endif
-#ifndef TAIL_SDMA
-#define TAIL_SDMA 1
+// the pass's last commit writes the status words to the pinned host area
+#ifndef STATUS_IN_COMMIT
+#define STATUS_IN_COMMIT 1
 #endif
 #ifndef CHUNK_MIN_TAIL
 #define CHUNK_MIN_TAIL 0  // 256-pod units: a stream's last chunk at least this long
@@ -2165,6 +2166,14 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         scored[c] = tm.mark(ss);
     }
     if (live_cap) OK(pass_init(sc));
+    // speculative slots: as many as the previous pass of this shape needed
+    // (consecutive passes over similar clusters stop alike), enqueued before
+    // the first status round trip; a slot whose walk is not halted exits at
+    // once.  Not with a communicator: every rank must issue the same slots.
+    const int spec = (!has_coll(ctx) && ctx->slot_hint_P == P && ctx->slot_hint_N == N) ? ctx->slot_hint : 0;
+    // (an injected stall, NAS_OPT_INJECT_STALL_MS, sits on st behind the
+    // pass: the host must wait on st then)
+    const bool status_in_commit = STATUS_IN_COMMIT && spec == 0 && ctx->opt_inject_stall_ms == 0;
     for (size_t c = 0; c < chunks.size(); ++c) {
         const int lo = chunks[c].first, hi = chunks[c].second;
         // the last chunk is merged and committed on its own scoring stream
@@ -2173,6 +2182,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         // cross-stream hop in front of its merge (the communicator is the
         // commit stream's: its collectives stay in one order)
         const bool tail = !one_stream && c + 1 == chunks.size();
+        const bool last = c + 1 == chunks.size();
         hipStream_t cs = sc;
         if (tail) {
             cs = ss2[c & 1];
@@ -2180,24 +2190,19 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         } else {
             HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
         }
+        // (merging the tail chunk locally before this wait, gated before its
+        // exchange / commit, measured within noise at G = 1 and 8:
+        // profiles/r04_ab_tail.txt)
         OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx)));
         hipEvent_t c0 = tm.fine(cs);
-        // the tail chunk's results go to the host by DMA copies behind its
-        // commit (the scoring is over, nothing delays them), not by the
-        // commit workgroup's own stores over the host link
-        const bool sdma = tail && TAIL_SDMA;
+        // the pass's last commit also writes the status words into the pinned
+        // host area when nothing follows it (no speculative slots): the host
+        // then waits for that commit alone, with no status copy behind it
         HIPCK(nas::launch_commit(cs, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
-                                 1, pub, zrow_ptr(ctx), sdma ? nullptr : stage,
-                                 (want_raw && !sdma) ? stage + P : nullptr));
-        if (sdma) {
-            HIPCK(hipMemcpyAsync(stage + lo, ctx->out_node.as<int32_t>() + lo, (size_t)(hi - lo) * 4,
-                                 hipMemcpyDeviceToHost, cs));
-            if (want_raw)
-                HIPCK(hipMemcpyAsync(stage + P + lo, ctx->out_cost_i.as<int32_t>() + lo,
-                                     (size_t)(hi - lo) * 4, hipMemcpyDeviceToHost, cs));
-        }
+                                 1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr,
+                                 last && status_in_commit ? hs : nullptr));
         tm.span(T_COMMIT, c0, tm.fine(cs));
         // the commit wrote this chunk's results into the pinned stage as it
         // ended, and the host unpacks them while later chunks still run
@@ -2209,11 +2214,6 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     if (!one_stream && ss2[(chunks.size() - 1) & 1] != st)
         HIPCK(hipStreamWaitEvent(st, tm.mark(ss2[(chunks.size() - 1) & 1]), 0));
     if (has_coll(ctx)) inject_stall(ctx, st);  // behind every collective of the pass
-    // speculative slots: as many as the previous pass of this shape needed
-    // (consecutive passes over similar clusters stop alike), enqueued before
-    // the first status round trip; a slot whose walk is not halted exits at
-    // once.  Not with a communicator: every rank must issue the same slots.
-    const int spec = (!has_coll(ctx) && ctx->slot_hint_P == P && ctx->slot_hint_N == N) ? ctx->slot_hint : 0;
     for (int r = 0; r < spec; ++r) OK(gathered_slot(ctx, tm, st, CH_SCORE, nullptr, P));
     if (spec > 0) {
         // behind the slots, all placements again: when they finished the walk,
@@ -2227,7 +2227,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     hipEvent_t t1 = nullptr;
     // status words in one copy: halt[0..2] = halt word, slot resumes, commit
     // rounds; halt[STATUS_INTS + 2] (slot control) = pods rescored
-    constexpr int NSTAT = nas::STATUS_INTS + 3, RESCORED = nas::STATUS_INTS + 2;
+    constexpr int NSTAT = nas::COMMIT_STATUS_WORDS, RESCORED = nas::STATUS_INTS + 2;
     auto fetch = [&]() -> int {
         HIPCK(hipMemcpyAsync(hs, halt, NSTAT * 4, hipMemcpyDeviceToHost, st));
         HIPCK(hipMemcpyAsync(stage, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost, st));
@@ -2255,13 +2255,17 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // host unpacks each chunk as its copy lands.  Values copied behind a commit
     // are final unless the walk halted there -- then (rare) more slots run and
     // everything is fetched and unpacked again.
-    HIPCK(hipMemcpyAsync(hs, halt, NSTAT * 4, hipMemcpyDeviceToHost, st));
-    t1 = tm.mark(st);
+    if (status_in_commit) {
+        t1 = landed.back().ev;  // the last commit wrote hs itself
+    } else {
+        HIPCK(hipMemcpyAsync(hs, halt, NSTAT * 4, hipMemcpyDeviceToHost, st));
+        t1 = tm.mark(st);
+    }
     for (const Landed &l : landed) {
         OK(wait_event(ctx, l.ev));
         unpack(l.lo, l.hi, stage);
     }
-    OK(wait_event(ctx, t1));  // t1 follows everything on st (the status copies)
+    OK(wait_event(ctx, t1));  // t1 follows the status words (copy, or the last commit)
     int checks = 0;
     if (spec > 0 && hs[0] < 0 && hs[1] > 0) {
         // speculative slots finished a walk that had halted: the per-chunk

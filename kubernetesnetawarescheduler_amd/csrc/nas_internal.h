@@ -287,7 +287,11 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
                          const int32_t *req, int Pp, int p_begin, int p_end, int32_t *cap, int N,
                          int32_t *out_node, int32_t *out_cost_i, int32_t *halt, int batch = 1,
                          int32_t *pub = nullptr, const uint8_t *zrow = nullptr,
-                         int32_t *stage_node = nullptr, int32_t *stage_cost = nullptr);
+                         int32_t *stage_node = nullptr, int32_t *stage_cost = nullptr,
+                         int32_t *stage_status = nullptr);
+// stage_status (batch 1): after the walk the commit copies the status words
+// status[0 .. COMMIT_STATUS_WORDS) there (pinned host memory)
+constexpr int COMMIT_STATUS_WORDS = STATUS_INTS + 3;
 // zrow[r] = 1 iff traffic row r (row_bytes bytes of WA) is all zero bytes and
 // has no overflow entries (ovf_ptr may be null): the pod's every cost is 0
 hipError_t launch_zero_rows(hipStream_t st, const void *WA, int64_t rows, int64_t row_bytes,

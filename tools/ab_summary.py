@@ -8,14 +8,15 @@ import os
 import sys
 
 
-def main(d, la="A", lb="B"):
+def main(d, *labels):
     for f in sorted(glob.glob(os.path.join(d, "[A-F]_*.json"))):
         try:
             p = json.load(open(f))
         except (ValueError, OSError):
             print(os.path.basename(f), "unreadable")
             continue
-        tag = {"A": la, "B": lb}.get(os.path.basename(f)[0], os.path.basename(f)[0])
+        k = os.path.basename(f)[0]
+        tag = labels["ABCDEF".index(k)] if "ABCDEF".index(k) < len(labels) else k
         rf = p.get("roofline", {})
         fr = p.get("fit_roofline", {})
         cf = p.get("configs", {})
