@@ -63,6 +63,9 @@ constexpr int PG_WIDE = 2;
 // SIMD of the same 128 x 64 shape, 160 KiB LDS double buffer), 17% fewer
 // staged bytes per MAC, for the main scoring pass of one large cluster
 constexpr int WIDE_PODS = 384;
+#ifndef COST_WIDE_SADDR
+#define COST_WIDE_SADDR 1
+#endif
 
 template <int DT>
 struct Mma;
@@ -95,6 +98,24 @@ struct Mma<NAS_DT_BF16> {
 __device__ __forceinline__ void glds16(const void *g, void *l) {
     __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)g,
                                      (void __attribute__((address_space(3))) *)l, 16, 0, 0);
+}
+
+// The same 16-byte LDS-DMA in its saddr form: a wave-uniform 64-bit base in
+// SGPRs plus a 32-bit per-lane offset, so every piece of a wave shares ONE
+// offset VGPR (the builtin keeps a 64-bit VGPR address per piece live across
+// the loop).  M0 (the LDS destination, wave-uniform) is saved and restored in
+// the statement.  hipcc does not count these loads: the K-loop retires them
+// with its explicit vmcnt(0) before each barrier.
+__device__ __forceinline__ unsigned lds_off(const void *p) {
+    return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ void glds16_s(const void *sbase, unsigned voff, unsigned ldsa) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(ldsa)
+                 : "memory");
 }
 
 __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
@@ -253,7 +274,11 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         if (pj >= (BM + BNK) / 8) return;
         const unsigned char *base = pj < BM / 8 ? Ag + (size_t)pj * 8 * Kb
                                                 : Bg + (size_t)(pj - BM / 8) * 8 * Kb;
+#if COST_WIDE_SADDR
+        glds16_s(base + k0, loff, __builtin_amdgcn_readfirstlane(lds_off(lds + buf * STG + pj * 8 * BKB)));
+#else
         glds16(base + k0 + loff, lds + buf * STG + pj * 8 * BKB);
+#endif
     };
     auto stageA = [&](int buf, int k0) {
         if constexpr (NWN == 6) {
