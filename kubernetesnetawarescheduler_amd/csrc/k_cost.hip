@@ -66,6 +66,12 @@ constexpr int WIDE_PODS = 384;
 #ifndef COST_WIDE_SADDR
 #define COST_WIDE_SADDR 1
 #endif
+#ifndef COST_XOR_FRAG
+#define COST_XOR_FRAG 1
+#endif
+#ifndef COST_NARROW_SADDR
+#define COST_NARROW_SADDR 1
+#endif
 
 template <int DT>
 struct Mma;
@@ -240,9 +246,20 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     auto bbuf = [&](int b) -> unsigned char * { return lds + b * STG + BM * BKB; };
     // one 1 KiB LDS-DMA piece (8 rows x 128 B) of operand A / B: piece j of
     // wave w fills rows (NW*j + w)*8 .. +8
+    // (saddr form, COST_NARROW_SADDR: rows r0 + l/8 of a piece all swizzle by
+    // (4 * (r0 / 8) + l / 16) & 7 = (4 * (w & 1) + l / 16) & 7 -- NW is even --,
+    // so one lane offset serves every piece of the wave, A and B alike)
+    const unsigned loffn = (unsigned)(srow_in * Kb) +
+                           ((unsigned)(sq ^ ((4 * (w & 1) + (srow_in >> 1)) & 7)) << 4);
     auto pieceA = [&](int buf, int k0, int j) {
         if (BM / 8 % NW && j * NW + w >= BM / 8) return;
         const int r0 = (j * NW + w) * 8;
+        if constexpr (COST_NARROW_SADDR && NW % 2 == 0) {
+            const int ru = __builtin_amdgcn_readfirstlane(r0);
+            glds16_s(Ag + (size_t)ru * Kb + k0, loffn,
+                     __builtin_amdgcn_readfirstlane(lds_off(abuf(buf) + r0 * BKB)));
+            return;
+        }
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
         glds16(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
@@ -256,6 +273,12 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     auto pieceB = [&](int buf, int k0, int j) {
         if (BNK / 8 % NW && j * NW + w >= BNK / 8) return;
         const int r0 = (j * NW + w) * 8;
+        if constexpr (!RMAP && COST_NARROW_SADDR && NW % 2 == 0) {
+            const int ru = __builtin_amdgcn_readfirstlane(r0);
+            glds16_s(Bg + (size_t)ru * Kb + k0, loffn,
+                     __builtin_amdgcn_readfirstlane(lds_off(bbuf(buf) + r0 * BKB)));
+            return;
+        }
         const int row = r0 + srow_in;
         const int c = sq ^ ((row >> 1) & 7);
         const unsigned char *src = RMAP ? WA + (size_t)bpod[j] * Kb : Bg + (size_t)row * Kb;
@@ -492,7 +515,23 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         const unsigned char *As = abuf(buf);
         const unsigned char *Bs = bbuf(buf);
         v4i a[2][4], bb[2][NI];
+        // fragment (kk, mi) of row r = base + mi * 32 + fr sits at r * BKB +
+        // ((2 kk + fh) ^ ((r >> 1) & 7)) * 16 = (row0 * BKB + ((fh ^ s) << 4)) ^
+        // (kk << 5) + mi * 4096 with s = (fr >> 1) & 7 (the same for every mi,
+        // ni and both operands): one lane offset per operand, an XOR per
+        // substep and immediate offsets (COST_XOR_FRAG)
         auto read = [&](int kk, v4i (&ra)[4], v4i (&rb)[NI]) {
+            if constexpr (COST_XOR_FRAG) {
+                const unsigned ao = ((unsigned)((wm * 128 + fr) * BKB) + (unsigned)((fh ^ ((fr >> 1) & 7)) << 4)) ^ (unsigned)(kk << 5);
+                const unsigned bo = ((unsigned)((wn * WPODS + fr) * BKB) + (unsigned)((fh ^ ((fr >> 1) & 7)) << 4)) ^ (unsigned)(kk << 5);
+#pragma unroll
+                for (int mi = 0; mi < 4; ++mi)
+                    ra[mi] = *reinterpret_cast<const v4i *>(As + ao + mi * 32 * BKB);
+#pragma unroll
+                for (int ni = 0; ni < NI; ++ni)
+                    rb[ni] = *reinterpret_cast<const v4i *>(Bs + bo + ni * 32 * BKB);
+                return;
+            }
             const int c = kk * 2 + fh;
 #pragma unroll
             for (int mi = 0; mi < 4; ++mi) {
