@@ -332,8 +332,17 @@ int prepare_split(nas_ctx *ctx) {
 // tails) and on batches of small clusters (C5: 5,000 pods = 13.02 wide tiles)
 // it loses, so those keep the 256 x 256 tile (profiles/r02_s4_ab_wide*.txt)
 constexpr int WIDE_MIN_PODS = 32768;
+#ifndef WIDE_BATCH
+#define WIDE_BATCH 1
+#endif
+#ifndef WIDE_SHARD
+#define WIDE_SHARD 0
+#endif
 bool wide_ok(const nas_ctx *ctx) {
-    return ctx->B == 1 && ctx->world == 1 && ctx->rehearse == 0 && ctx->Pp >= WIDE_MIN_PODS;
+    const bool shard = ctx->world > 1 || ctx->rehearse > 1;
+    if (shard && !WIDE_SHARD) return false;
+    if (ctx->B > 1) return WIDE_BATCH && !shard;
+    return ctx->Pp >= WIDE_MIN_PODS || shard;
 }
 int tile_pods(const nas_ctx *ctx) {
     return wide_ok(ctx) ? nas::cost_tile_pods(ctx->dtype == NAS_DT_F32 ? NAS_DT_BF16 : ctx->dtype)
@@ -705,7 +714,7 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     // cost launches each of them waited ~100 us for a cost workgroup to
     // drain (G = 8 rehearsal 1.53 vs 1.34 ms per pass in round 2:
     // profiles/r03_g8_timeline_before.txt, r03_ab_fuse_shard.txt)
-    const bool fuse = NAS_FUSE_SHARD || ctx->world == 1;
+    const bool fuse = NAS_FUSE_SHARD || ctx->world == 1 || wide_ok(ctx);
     const nas::FitSrc fit{cap, v.req, ctx->N, ctx->Nloc0, ctx->Nloc};
     hipEvent_t e0 = tm.fine(st);
     if (!fuse)
@@ -1063,7 +1072,8 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     // other stream still has undispatched workgroups to fill the CUs (with
     // equal chunks both streams drained together: ~20 us of idle CUs per
     // chunk pair in the C3 pass timeline)
-    if (tile_pods(ctx) != nas::COST_BN) tiles = c == 1 ? CHUNK_TILES_WIDE / 2 : CHUNK_TILES_WIDE;
+    if (tile_pods(ctx) != nas::COST_BN && ctx->world == 1)
+        tiles = c == 1 ? CHUNK_TILES_WIDE / 2 : CHUNK_TILES_WIDE;
     // a pass whose pods fit one big chunk (C2: 40 pod tiles on 4 node tiles)
     // is one chunk: pipelining its short tail would save less than the
     // cross-stream hops and launches it adds (device time 0.96 -> 0.92 ms, C2)
@@ -1121,7 +1131,7 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
 std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
     std::vector<std::pair<int, int>> chunks;
     const int P = ctx->P;
-    const bool wide = tile_pods(ctx) != nas::COST_BN;
+    const bool wide = tile_pods(ctx) != nas::COST_BN && ctx->world == 1;
     // a node shard with few node tiles: equal chunks of ~CHUNK_WORKGROUPS
     // cost workgroups (chunk_pods mode 2); balanced the same way only when
     // built with CHUNK_BALANCE_SHARD=1
