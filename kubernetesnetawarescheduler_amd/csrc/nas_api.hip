@@ -332,6 +332,9 @@ int prepare_split(nas_ctx *ctx) {
 // tails) and on batches of small clusters (C5: 5,000 pods = 13.02 wide tiles)
 // it loses, so those keep the 256 x 256 tile (profiles/r02_s4_ab_wide*.txt)
 constexpr int WIDE_MIN_PODS = 32768;
+#ifndef RESERVE_CUS
+#define RESERVE_CUS 0  // CUs per XCD kept for the commit stream (nas_create)
+#endif
 #ifndef WIDE_BATCH
 #define WIDE_BATCH 1
 #endif
@@ -1359,6 +1362,39 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
         delete ctx;
         return NAS_ERR_HIP;
     }
+#if RESERVE_CUS
+    // RESERVE_CUS per XCD for the commit stream (the merge / exchange /
+    // commit chain beside a cost kernel that fills every CU it runs on).  The
+    // CU-mask bit i is CU i / 8 of XCD i % 8 (tools/cumask_probe.hip), and an
+    // XCD whose bits are all clear runs on all its CUs: every mask keeps at
+    // least one CU of every XCD.
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            ncu >= 64) {
+            const int words = (ncu + 31) / 32;
+            std::vector<uint32_t> ms(words, 0), mc(words, 0);
+            for (int b = 0; b < ncu; ++b) {
+                const bool res = b < 8 * RESERVE_CUS;
+                (res ? mc : ms)[b / 32] |= 1u << (b % 32);
+            }
+            hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;
+            if (hipExtStreamCreateWithCUMask(&s1, words, ms.data()) == hipSuccess &&
+                hipExtStreamCreateWithCUMask(&s2, words, ms.data()) == hipSuccess &&
+                hipExtStreamCreateWithCUMask(&s3, words, mc.data()) == hipSuccess) {
+                (void)hipStreamDestroy(ctx->stream);
+                (void)hipStreamDestroy(ctx->stream2);
+                (void)hipStreamDestroy(ctx->stream_commit);
+                ctx->stream = s1;
+                ctx->stream2 = s2;
+                ctx->stream_commit = s3;
+            } else {
+                for (hipStream_t x : {s1, s2, s3})
+                    if (x) (void)hipStreamDestroy(x);
+            }
+        }
+    }
+#endif
     *out = ctx;
     return NAS_OK;
 }
