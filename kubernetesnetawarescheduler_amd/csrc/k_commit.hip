@@ -83,6 +83,11 @@ __device__ __forceinline__ void retire_window();
 __device__ __forceinline__ void retire_oldest(int younger);
 constexpr int LDS_CAP_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 12;  // + cap_to_lds padding
 constexpr int NO_POD = 0x7fffffff;
+// k_commit_w's side-by-side capacity image: 16 B per node beside the ring
+constexpr int AOS_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 16;
+#ifndef COMMIT_AOS
+#define COMMIT_AOS 1
+#endif
 // walks of up to this many pods run in one wave (k_commit_w): fewer, exact
 // stops for herds on small clusters (C2: 0.67 -> 0.62 ms per pass; with the
 // zero-traffic scan and no rescore left, 0.55 vs 0.63 ms for k_commit); longer
@@ -116,8 +121,8 @@ constexpr int ZSCAN_L2 = 16;
 // `from` (per pod, -1 at first): where this pod's previous scan stopped -- the
 // nodes below it did not fit then and capacity only shrinks between picks
 // (a round's failed reservations are undone before the next round picks)
-template <bool LDS_CAP, typename LD>
-__device__ __forceinline__ int zero_row_scan(u64 bound, int r0, int r1, int r2, int N, LD &&ld,
+template <bool LDS_CAP, typename LD3>
+__device__ __forceinline__ int zero_row_scan(u64 bound, int r0, int r1, int r2, int N, LD3 &&ld3,
                                              int &from) {
     const int nb = (int)(unsigned)bound + 1;
     const int n0 = max(nb, from);
@@ -129,8 +134,8 @@ __device__ __forceinline__ int zero_row_scan(u64 bound, int r0, int r1, int r2, 
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int m = min(n + j, n1 - 1);
-            const int a = ld(m), b = ld(N + m), c = ld(2 * N + m);
-            fit |= (unsigned)((r0 <= a) & (r1 <= b) & (r2 <= c) & (n + j < n1)) << j;
+            const int4 v = ld3(m);
+            fit |= (unsigned)((r0 <= v.x) & (r1 <= v.y) & (r2 <= v.z) & (n + j < n1)) << j;
         }
         if (fit) {
             from = n + __builtin_ctz(fit);
@@ -369,7 +374,8 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             if (done) choice = -1;
             bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
             if (COMMIT_ZSCAN && rescore && zrow && zrow[i] && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
-                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld, zfrom);
+                auto ld3 = [&](int n) { return make_int4(ld(n), ld(N + n), ld(2 * N + n), 0); };
+                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld3, zfrom);
                 if (z != -2) {
                     rescore = false;
                     choice = z;  // -1: nothing fits (NAS_EMPTY)
@@ -508,7 +514,10 @@ __device__ __forceinline__ void glds(const void *g, unsigned lds) {
                      : "memory");
 }
 
-template <bool LDS_CAP>
+// AOS (capacity in LDS only): node n's three resources side by side,
+// {cpu, mem, pods, 0} at capl + 4 n, so a candidate check is ONE 16-byte LDS
+// read instead of three (up to 8,656 nodes beside the prefetch ring)
+template <bool LDS_CAP, bool AOS = false>
 __global__ void __launch_bounds__(64)
 k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
            const int *__restrict__ req, int Pp, int p_begin, int p_end, int *__restrict__ cap_g,
@@ -535,8 +544,16 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         return;
     }
     if (resume) p_begin = h;
-    if (LDS_CAP) cap_to_lds(cap_g, capl, 3 * N, 0, 1);
+    static_assert(!AOS || LDS_CAP, "the side-by-side layout is an LDS image");
+    if constexpr (AOS) {
+        for (int i = lane; i < N; i += 64)
+            *reinterpret_cast<int4 *>(capl + 4 * i) = make_int4(cap_g[i], cap_g[N + i], cap_g[2 * N + i], 0);
+    } else if (LDS_CAP) {
+        cap_to_lds(cap_g, capl, 3 * N, 0, 1);
+    }
     int *cap = LDS_CAP ? capl : cap_g;
+    // resource r of node n
+    auto ci = [&](int r, int n) { return AOS ? 4 * n + r : r * N + n; };
     struct Pod {
         u64 k[KC];
         u64 bound;
@@ -553,12 +570,17 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         if (LDS_CAP) return cap[idx];
         return __hip_atomic_load(cap + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
+    auto ld3 = [&](int n) -> int4 {
+        if constexpr (AOS) return *reinterpret_cast<const int4 *>(cap + 4 * n);
+        return make_int4(ld(n), ld(N + n), ld(2 * N + n), 0);
+    };
     Pod cur;
     if (lane == 0 && h >= 0) {
         halt[0] = -1;
         if (resume) halt[1] += 1;
     }
-    unsigned char *pf = reinterpret_cast<unsigned char *>(smem) + (LDS_CAP ? (3 * N * 4 + 255) / 256 * 256 : 0);
+    unsigned char *pf = reinterpret_cast<unsigned char *>(smem) +
+                        (AOS ? (16 * N + 255) / 256 * 256 : LDS_CAP ? (3 * N * 4 + 255) / 256 * 256 : 0);
     const unsigned char *zsrc = zrow ? zrow : reinterpret_cast<const unsigned char *>(req);
     // window wbase's lists into ring slot `slot` (9 LDS-DMA instructions; lanes
     // past the data re-read its last bytes into the slot's idle space)
@@ -612,7 +634,8 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 bool more = k0 != KEY_INVALID && k0 <= cur.bound;
                 if (more) {
                     const int n = (int)(unsigned)k0;
-                    if ((int)(cur.r0 <= ld(n)) & (int)(cur.r1 <= ld(N + n)) & (int)(cur.r2 <= ld(2 * N + n))) {
+                    const int4 v = ld3(n);
+                    if ((int)(cur.r0 <= v.x) & (int)(cur.r1 <= v.y) & (int)(cur.r2 <= v.z)) {
                         choice = n;
                         ccost = (unsigned)(k0 >> 32);
                         more = false;
@@ -630,8 +653,8 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                         const u64 k = cur.k[j];
                         const bool usable = k != KEY_INVALID && k <= cur.bound;
                         const int n = usable ? (int)(unsigned)k : 0;
-                        const int a = ld(n), b = ld(N + n), c = ld(2 * N + n);
-                        okm |= (unsigned)(usable & (cur.r0 <= a) & (cur.r1 <= b) & (cur.r2 <= c)) << j;
+                        const int4 v = ld3(n);
+                        okm |= (unsigned)(usable & (cur.r0 <= v.x) & (cur.r1 <= v.y) & (cur.r2 <= v.z)) << j;
                     }
 #pragma unroll
                     for (int j = KC - 1; j >= 1; --j)  // constant indices (no scratch array)
@@ -647,7 +670,8 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                     const u64 k = cur.k[j];
                     if (k == KEY_INVALID || k > cur.bound) break;
                     const int n = (int)(unsigned)k;
-                    if (cur.r0 <= ld(n) && cur.r1 <= ld(N + n) && cur.r2 <= ld(2 * N + n)) {
+                    const int4 v = ld3(n);
+                    if (cur.r0 <= v.x && cur.r1 <= v.y && cur.r2 <= v.z) {
                         choice = n;
                         ccost = (unsigned)(k >> 32);
                         break;
@@ -656,7 +680,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             }
             bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
             if (COMMIT_ZSCAN && rescore && cur.z && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
-                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld, zfrom);
+                const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld3, zfrom);
                 if (z != -2) {
                     rescore = false;
                     choice = z;  // -1: nothing fits (NAS_EMPTY)
@@ -665,7 +689,7 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             }
             bool g0 = false, g1 = false, g2 = false;
             if (choice >= 0)
-                reserve3<LDS_CAP>(cap + choice, cap + N + choice, cap + 2 * N + choice, cur.r0,
+                reserve3<LDS_CAP>(cap + ci(0, choice), cap + ci(1, choice), cap + ci(2, choice), cur.r0,
                                   cur.r1, cur.r2, g0, g1, g2);
             const bool bad = rescore || (choice >= 0 && !(g0 && g1 && g2));
             const u64 bm = __ballot(bad);
@@ -681,9 +705,9 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             const int sl = (int)__builtin_ctzll(bm);
             const int s = base + sl;
             if (!done && lane >= sl && choice >= 0) {
-                if (g0) atomicAdd(cap + choice, cur.r0);
-                if (g1) atomicAdd(cap + N + choice, cur.r1);
-                if (g2) atomicAdd(cap + 2 * N + choice, cur.r2);
+                if (g0) atomicAdd(cap + ci(0, choice), cur.r0);
+                if (g1) atomicAdd(cap + ci(1, choice), cur.r1);
+                if (g2) atomicAdd(cap + ci(2, choice), cur.r2);
             }
             if (!done && lane < sl) {
                 out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
@@ -699,10 +723,11 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             if (lane == sl) {
                 // pod s against the capacity left by the pods below it
                 const int n = choice;
-                if (cur.r0 <= ld(n) && cur.r1 <= ld(N + n) && cur.r2 <= ld(2 * N + n)) {
-                    atomicSub(cap + n, cur.r0);
-                    atomicSub(cap + N + n, cur.r1);
-                    atomicSub(cap + 2 * N + n, cur.r2);
+                const int4 v = ld3(n);
+                if (cur.r0 <= v.x && cur.r1 <= v.y && cur.r2 <= v.z) {
+                    atomicSub(cap + ci(0, n), cur.r0);
+                    atomicSub(cap + ci(1, n), cur.r1);
+                    atomicSub(cap + ci(2, n), cur.r2);
                     out_node[i] = n;
                     out_cost[i] = ccost;
                     publish(n, cur);
@@ -729,8 +754,16 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     __syncthreads();  // (one wave: every lane's placements written)
     to_stage(out_node, out_cost, stage_node ? stage_node + (size_t)cb * p_end : nullptr,
              stage_cost ? stage_cost + (size_t)cb * p_end : nullptr, p_begin, p_end, lane, 64);
-    if (LDS_CAP)
+    if constexpr (AOS) {
+        for (int i = lane; i < N; i += 64) {
+            const int4 v = *reinterpret_cast<const int4 *>(capl + 4 * i);
+            cap_g[i] = v.x;
+            cap_g[N + i] = v.y;
+            cap_g[2 * N + i] = v.z;
+        }
+    } else if (LDS_CAP) {
         for (int i = lane; i < 3 * N; i += 64) cap_g[i] = capl[i];
+    }
 }
 
 }  // namespace
@@ -751,7 +784,16 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
     if (Pp <= ONE_WAVE_MAX_PODS) {
-        if (N <= LDS_CAP_MAX_NODES) {
+        if (COMMIT_AOS && N <= AOS_MAX_NODES) {
+            const size_t lds = round_up(16 * (size_t)N, 256) + PF_BYTES;
+            static std::atomic<unsigned long long> attr{0};
+            hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit_w<true, true>),
+                                        LDS_DYN_MAX, attr);
+            if (e != hipSuccess) return e;
+            k_commit_w<true, true><<<batch, 64, lds, st>>>(ck, cb, req, Pp, p_begin, p_end, cap, N,
+                                                           out_node, oc, halt, nullptr, zrow, stage_node,
+                                                           sc, stage_status);
+        } else if (N <= LDS_CAP_MAX_NODES) {
             const size_t lds = round_up(3 * (size_t)N * 4, 256) + PF_BYTES;  // cap_to_lds pieces + ring
             static std::atomic<unsigned long long> attr{0};
             hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit_w<true>),
