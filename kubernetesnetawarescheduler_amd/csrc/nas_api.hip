@@ -332,14 +332,18 @@ int prepare_split(nas_ctx *ctx) {
 // tails) and on batches of small clusters (C5: 5,000 pods = 13.02 wide tiles)
 // it loses, so those keep the 256 x 256 tile (profiles/r02_s4_ab_wide*.txt)
 constexpr int WIDE_MIN_PODS = 32768;
-#ifndef RESERVE_CUS
-#define RESERVE_CUS 0  // CUs per XCD kept for the commit stream (nas_create)
+// On a node shard (world > 1) the scoring streams leave RESERVE_SHARD_CUS
+// CUs per XCD to the commit stream (set_stream_masks), so the merge /
+// exchange / commit chain runs beside the wide cost tile instead of waiting
+// for one of its workgroups to drain (profiles/r04_ab_reserve.txt)
+#ifndef RESERVE_SHARD_CUS
+#define RESERVE_SHARD_CUS 2  // per XCD; 3 from 8 ranks up (shard_reserve)
 #endif
 #ifndef WIDE_BATCH
 #define WIDE_BATCH 1
 #endif
 #ifndef WIDE_SHARD
-#define WIDE_SHARD 0
+#define WIDE_SHARD 1
 #endif
 bool wide_ok(const nas_ctx *ctx) {
     const bool shard = ctx->world > 1 || ctx->rehearse > 1;
@@ -1362,39 +1366,6 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
         delete ctx;
         return NAS_ERR_HIP;
     }
-#if RESERVE_CUS
-    // RESERVE_CUS per XCD for the commit stream (the merge / exchange /
-    // commit chain beside a cost kernel that fills every CU it runs on).  The
-    // CU-mask bit i is CU i / 8 of XCD i % 8 (tools/cumask_probe.hip), and an
-    // XCD whose bits are all clear runs on all its CUs: every mask keeps at
-    // least one CU of every XCD.
-    {
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-            ncu >= 64) {
-            const int words = (ncu + 31) / 32;
-            std::vector<uint32_t> ms(words, 0), mc(words, 0);
-            for (int b = 0; b < ncu; ++b) {
-                const bool res = b < 8 * RESERVE_CUS;
-                (res ? mc : ms)[b / 32] |= 1u << (b % 32);
-            }
-            hipStream_t s1 = nullptr, s2 = nullptr, s3 = nullptr;
-            if (hipExtStreamCreateWithCUMask(&s1, words, ms.data()) == hipSuccess &&
-                hipExtStreamCreateWithCUMask(&s2, words, ms.data()) == hipSuccess &&
-                hipExtStreamCreateWithCUMask(&s3, words, mc.data()) == hipSuccess) {
-                (void)hipStreamDestroy(ctx->stream);
-                (void)hipStreamDestroy(ctx->stream2);
-                (void)hipStreamDestroy(ctx->stream_commit);
-                ctx->stream = s1;
-                ctx->stream2 = s2;
-                ctx->stream_commit = s3;
-            } else {
-                for (hipStream_t x : {s1, s2, s3})
-                    if (x) (void)hipStreamDestroy(x);
-            }
-        }
-    }
-#endif
     *out = ctx;
     return NAS_OK;
 }
@@ -2512,6 +2483,60 @@ int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out
 }
 
 // ---------------------------------------------------------------- multi-GPU
+namespace {
+// CUs per XCD kept for the commit stream on a node shard of `world` ranks:
+// same-box A/B (profiles/r04_ab_reserve.txt), rank-0 rehearsal ms per pass at
+// reserve 0 (narrow tile) / 2 / 3 / 4: G = 2 4.13-4.21 / 3.92-3.97 /
+// 3.96-4.00 / 3.99-4.03, G = 4 2.27-2.29 / 2.19-2.20 / 2.20-2.22 /
+// 2.16-2.20, G = 8 1.28-1.32 / 1.27-1.28 / 1.24-1.26 / 1.24-1.29
+int shard_reserve(int world) {
+    if (world <= 1 || !WIDE_SHARD) return 0;
+    return world >= 8 ? RESERVE_SHARD_CUS + 1 : RESERVE_SHARD_CUS;
+}
+// Recreate the context's three streams: reserve > 0 keeps `reserve` CUs of
+// every XCD for the commit stream alone and the rest for the two scoring
+// streams (hipExtStreamCreateWithCUMask: mask bit i is CU i / 8 of XCD i % 8,
+// tools/cumask_probe.hip; an XCD whose bits are all clear would run on ALL its
+// CUs, so every mask keeps CUs on every XCD); reserve 0 restores plain
+// streams.  Only between calls (nothing in flight).
+int set_stream_masks(nas_ctx *ctx, int reserve) {
+    if (reserve == ctx->cu_reserve) return NAS_OK;
+    int ncu = 0;
+    HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    if (reserve > 0 && (ncu % 8 || ncu / 8 <= 2 * reserve)) reserve = 0;  // not an 8-XCD part
+    if (reserve == ctx->cu_reserve) return NAS_OK;
+    for (hipStream_t s : {ctx->stream, ctx->stream2, ctx->stream_commit}) HIPCK(hipStreamSynchronize(s));
+    hipStream_t ns[3] = {nullptr, nullptr, nullptr};
+    hipError_t e = hipSuccess;
+    if (reserve > 0) {
+        const int words = (ncu + 31) / 32;
+        std::vector<uint32_t> ms(words, 0), mc(words, 0);
+        for (int b = 0; b < ncu; ++b) (b < 8 * reserve ? mc : ms)[b / 32] |= 1u << (b % 32);
+        for (int i = 0; i < 3 && e == hipSuccess; ++i)
+            e = hipExtStreamCreateWithCUMask(&ns[i], (uint32_t)words, i == 2 ? mc.data() : ms.data());
+    } else {
+        int lo = 0, hi = 0;
+        e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&ns[0], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&ns[1], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&ns[2], hipStreamNonBlocking, hi);
+    }
+    if (e != hipSuccess) {
+        for (hipStream_t s : ns)
+            if (s) (void)hipStreamDestroy(s);
+        return nas::hip_fail(ctx, e, "set_stream_masks");
+    }
+    (void)hipStreamDestroy(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream2);
+    (void)hipStreamDestroy(ctx->stream_commit);
+    ctx->stream = ns[0];
+    ctx->stream2 = ns[1];
+    ctx->stream_commit = ns[2];
+    ctx->cu_reserve = reserve;
+    return NAS_OK;
+}
+}  // namespace
+
 int nas_comm_unique_id(uint8_t id_out[128]) {
     NAS_RANGE("nas_comm_unique_id");
     if (!id_out) return NAS_ERR_ARG;
@@ -2788,7 +2813,7 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     ctx->comm = reinterpret_cast<ncclComm *>(st->kids[0]);
     ctx->comm2 = reinterpret_cast<ncclComm *>(st->kids[1]);
     ctx->comm_c = reinterpret_cast<ncclComm *>(st->kids[2]);
-    return NAS_OK;
+    return set_stream_masks(ctx, shard_reserve(eff_world));
 }
 
 int nas_local_group_create(int32_t world, nas_local_group **out) {
@@ -2842,7 +2867,7 @@ int nas_comm_init_local(nas_ctx *ctx, nas_local_group *group, int32_t rank) {
     ctx->lg_peers = 0;
     ctx->rank = rank;
     ctx->world = world;
-    return NAS_OK;
+    return set_stream_masks(ctx, shard_reserve(world));
 }
 
 int nas_set_shard(nas_ctx *ctx, int32_t rank, int32_t world) {

@@ -95,6 +95,7 @@ struct nas_ctx {
     hipStream_t stream = nullptr;      // main stream (uploads, scoring, results)
     hipStream_t stream2 = nullptr;     // second scoring stream (chunk tails overlap)
     hipStream_t stream_commit = nullptr;  // commit walks, pipelined behind scoring
+    int32_t cu_reserve = 0;               // CUs per XCD kept for stream_commit (set_stream_masks)
     std::string err;
     hipEvent_t ev[12] = {};
     nas_timings timings = {};
