@@ -27,9 +27,9 @@ def cdiv(a, b):
 
 def grid_x(nodes, pods, batch=1):
     """grid x (threads) of a full launch: the wide tile (256 x 384, 768
-    threads) for one cluster of >= 32,768 padded pods, else 256 x 256 / 512
-    (nas_api.hip wide_ok)."""
-    if batch == 1 and cdiv(pods, BN) * BN >= 32768:
+    threads) for one cluster of >= 32,768 padded pods or any cluster batch,
+    else 256 x 256 / 512 (nas_api.hip wide_ok)."""
+    if batch > 1 or cdiv(pods, BN) * BN >= 32768:
         return cdiv(nodes, BM) * cdiv(cdiv(pods, BN) * BN, 384) * 768
     return cdiv(nodes, BM) * cdiv(pods, BN) * 512
 
