@@ -55,7 +55,10 @@ constexpr int BKB = COST_BKB; // bytes of K per LDS stage (full 128-byte lines)
 // variants of this kernel (other pipelines, schedules, one wave per SIMD,
 // cache policies) live in tools/k_cost_diag.hip.
 constexpr int PG_NARROW = 4;
-constexpr int PG_WIDE = 2;
+#ifndef COST_PG_WIDE
+#define COST_PG_WIDE 2
+#endif
+constexpr int PG_WIDE = COST_PG_WIDE;
 // wave layouts: NWN = 4 -> 256 x 256 per 8-wave workgroup (2 node halves x 4
 // pod quarters, each wave 128 nodes x 64 pods = 4 x 2 MFMA 32x32 tiles, 128
 // accumulator registers, two waves per SIMD, 128 KiB LDS double buffer);
