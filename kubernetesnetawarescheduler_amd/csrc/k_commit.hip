@@ -83,6 +83,19 @@ __device__ __forceinline__ void retire_window();
 __device__ __forceinline__ void retire_oldest(int younger);
 constexpr int LDS_CAP_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 12;  // + cap_to_lds padding
 constexpr int NO_POD = 0x7fffffff;
+// COMMIT_PROF (diagnostic builds only): k_commit_w prints its shader-clock
+// cycles per phase at the end of every walk
+#ifndef COMMIT_PROF
+#define COMMIT_PROF 0
+#endif
+#if COMMIT_PROF
+#define CPROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define CPROF_ADD(acc, a, b) acc += (b) - (a)
+#else
+#define CPROF_T(v)
+#define CPROF_ADD(acc, a, b)
+#endif
+
 // k_commit_w's side-by-side capacity image: 16 B per node beside the ring
 constexpr int AOS_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 16;
 #ifndef COMMIT_AOS
@@ -131,12 +144,15 @@ __device__ __forceinline__ int zero_row_scan(u64 bound, int r0, int r1, int r2, 
     // re-reads n1 - 1 and is never taken)
     for (int n = n0; n < n1; n += 8) {
         unsigned fit = 0;
+        int4 v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int m = min(n + j, n1 - 1);
-            const int4 v = ld3(m);
-            fit |= (unsigned)((r0 <= v.x) & (r1 <= v.y) & (r2 <= v.z) & (n + j < n1)) << j;
-        }
+        for (int j = 0; j < 8; ++j) v[j] = ld3(min(n + j, n1 - 1));
+        // the 8 reads issue back to back (hipcc otherwise waits for each
+        // before the next: 8 LDS round trips per step)
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            fit |= (unsigned)((r0 <= v[j].x) & (r1 <= v[j].y) & (r2 <= v[j].z) & (n + j < n1)) << j;
         if (fit) {
             from = n + __builtin_ctz(fit);
             return from;
@@ -189,12 +205,15 @@ template <bool LDS_CAP>
 __device__ __forceinline__ void reserve3(int *c0, int *c1, int *c2, int r0, int r1, int r2,
                                          bool &g0, bool &g1, bool &g2) {
     if (r0 <= FETCH_SUB_MAX && r1 <= FETCH_SUB_MAX && r2 <= FETCH_SUB_MAX) {
-        const int p0 = r0 ? atomicSub(c0, r0) : 0;
-        const int p1 = r1 ? atomicSub(c1, r1) : 0;
-        const int p2 = r2 ? atomicSub(c2, r2) : 0;
-        g0 = p0 >= r0;
-        g1 = p1 >= r1;
-        g2 = p2 >= r2;
+        // all three subtractions in flight together (a zero request subtracts
+        // nothing and is granted whatever it reads)
+        const int p0 = atomicSub(c0, r0);
+        const int p1 = atomicSub(c1, r1);
+        const int p2 = atomicSub(c2, r2);
+        __builtin_amdgcn_sched_group_barrier(0x80, 3, 0);
+        g0 = r0 == 0 || p0 >= r0;
+        g1 = r1 == 0 || p1 >= r1;
+        g2 = r2 == 0 || p2 >= r2;
         if (!g0) atomicAdd(c0, r0);
         if (!g1) atomicAdd(c1, r1);
         if (!g2) atomicAdd(c2, r2);
@@ -621,11 +640,17 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     take(0, p_begin);
     int round = 0;
     int stop = p_end;
+#if COMMIT_PROF
+    unsigned long long c_pick = 0, c_z = 0, c_resv = 0, c_fin = 0, c_win = 0, c_conf = 0;
+    int n_z = 0, n_zsteps = 0, n_zmax = 0, n_zrounds = 0;
+    CPROF_T(c_start);
+#endif
     for (int base = p_begin, w = 0;; ++w) {
         const int i = base + lane;
         bool done = i >= p_end;
         int zfrom = -1;  // zero-traffic scan resume point (zero_row_scan)
         while (true) {
+            CPROF_T(t0);
             int choice = -1;
             unsigned ccost = 0;
             if (!done && COMMIT_BATCH) {
@@ -648,13 +673,21 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 // fitting bit is the sequential choice.
                 if (__ballot(more) && more) {
                     unsigned okm = 0;
+                    int4 v[KC];
 #pragma unroll
                     for (int j = 1; j < KC; ++j) {
                         const u64 k = cur.k[j];
                         const bool usable = k != KEY_INVALID && k <= cur.bound;
-                        const int n = usable ? (int)(unsigned)k : 0;
-                        const int4 v = ld3(n);
-                        okm |= (unsigned)(usable & (cur.r0 <= v.x) & (cur.r1 <= v.y) & (cur.r2 <= v.z)) << j;
+                        v[j] = ld3(usable ? (int)(unsigned)k : 0);
+                    }
+                    // the 7 reads back to back (hipcc otherwise keeps two in flight)
+                    __builtin_amdgcn_sched_group_barrier(0x100, KC - 1, 0);
+#pragma unroll
+                    for (int j = 1; j < KC; ++j) {
+                        const u64 k = cur.k[j];
+                        const bool usable = k != KEY_INVALID && k <= cur.bound;
+                        okm |= (unsigned)(usable & (cur.r0 <= v[j].x) & (cur.r1 <= v[j].y) &
+                                          (cur.r2 <= v[j].z)) << j;
                     }
 #pragma unroll
                     for (int j = KC - 1; j >= 1; --j)  // constant indices (no scratch array)
@@ -679,6 +712,15 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                 }
             }
             bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
+            CPROF_T(t1);
+            CPROF_ADD(c_pick, t0, t1);
+#if COMMIT_PROF
+            n_z += __builtin_popcountll(__ballot(COMMIT_ZSCAN && rescore && cur.z &&
+                                                 (unsigned)(cur.bound >> 32) == ZERO_COST_KEY));
+#endif
+#if COMMIT_PROF
+            int zs0 = max((int)(unsigned)cur.bound + 1, zfrom);
+#endif
             if (COMMIT_ZSCAN && rescore && cur.z && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
                 const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld3, zfrom);
                 if (z != -2) {
@@ -686,7 +728,25 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                     choice = z;  // -1: nothing fits (NAS_EMPTY)
                     ccost = ZERO_COST_KEY;
                 }
+#if COMMIT_PROF
+                zs0 = (zfrom - zs0) / 8 + 1;
+#endif
+            } else {
+#if COMMIT_PROF
+                zs0 = 0;
+#endif
             }
+#if COMMIT_PROF
+            {
+                int mx = zs0;
+                for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+                n_zsteps += mx;
+                n_zmax = max(n_zmax, mx);
+                n_zrounds += mx > 0;
+            }
+#endif
+            CPROF_T(t2);
+            CPROF_ADD(c_z, t1, t2);
             bool g0 = false, g1 = false, g2 = false;
             if (choice >= 0)
                 reserve3<LDS_CAP>(cap + ci(0, choice), cap + ci(1, choice), cap + ci(2, choice), cur.r0,
@@ -694,12 +754,16 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             const bool bad = rescore || (choice >= 0 && !(g0 && g1 && g2));
             const u64 bm = __ballot(bad);
             ++round;
+            CPROF_T(t3);
+            CPROF_ADD(c_resv, t2, t3);
             if (bm == 0) {  // no conflict: every pending pod of the window commits
                 if (!done) {
                     out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
                     out_cost[i] = ccost;
                     publish(choice, cur);
                 }
+                CPROF_T(t4);
+                CPROF_ADD(c_fin, t3, t4);
                 break;
             }
             const int sl = (int)__builtin_ctzll(bm);
@@ -734,8 +798,11 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                     done = true;
                 }
             }
+            CPROF_T(t5);
+            CPROF_ADD(c_conf, t3, t5);
         }
         if (stop < p_end || base + 64 >= p_end) break;
+        CPROF_T(tw0);
         // window w+1 (slot (w+1) % 4): windows w+2, w+3 may stay in flight
         younger = 0;
         for (int j = 2; j <= COMMIT_AHEAD; ++j) younger += base + 64 * j < p_end;
@@ -744,8 +811,18 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         base += 64;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot w % 4's reads done
         issue(base + 64 * COMMIT_AHEAD, (w + 1 + COMMIT_AHEAD) & 3);  // window w+1+AHEAD
+        CPROF_T(tw1);
+        CPROF_ADD(c_win, tw0, tw1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no untracked load outlives the walk
+#if COMMIT_PROF
+    CPROF_T(c_end);
+    if (lane == 0)
+        printf("CPROF pods=%d rounds=%d zpods=%d zsteps=%d zmax=%d zrounds=%d total=%llu pick=%llu "
+               "zscan=%llu reserve=%llu commit_fast=%llu conflict=%llu window=%llu\n", p_end - p_begin,
+               round, n_z, n_zsteps, n_zmax, n_zrounds, c_end - c_start, c_pick, c_z, c_resv, c_fin,
+               c_conf, c_win);
+#endif
     if (lane == 0) {
         if (stop < p_end) *halt = stop;
         halt[2] += round;
