@@ -2180,7 +2180,9 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     for (size_t c = 0; c < chunks.size(); ++c) {
         hipStream_t ss = ss2[c & 1];
         OK(score_range(ctx, tm, chunks[c].first, chunks[c].second, ss, score_cap, nullptr, false));
-        scored[c] = tm.mark(ss);
+        // (one stream: nothing waits on it -- every event record or wait is a
+        // packet the queue processes between two kernels)
+        scored[c] = one_stream ? nullptr : tm.mark(ss);
     }
     if (live_cap) OK(pass_init(sc));
     // speculative slots: as many as the previous pass of this shape needed
@@ -2204,7 +2206,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         if (tail) {
             cs = ss2[c & 1];
             HIPCK(hipStreamWaitEvent(cs, tm.mark(sc), 0));
-        } else {
+        } else if (!one_stream) {
             HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
         }
         // (merging the tail chunk locally before this wait, gated before its
