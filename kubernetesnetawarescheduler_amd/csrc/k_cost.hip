@@ -785,7 +785,12 @@ k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_list
         long long stride, long long bstride, int src_p0, int p0, int np,
         u64 *__restrict__ dst, u64 *__restrict__ dst_bound, int dst_p0,
         const int *__restrict__ dyn_start, int dyn_hi, int dyn_flags, long long dst_cs,
-        const int *__restrict__ dyn_hi_ptr, const int *__restrict__ dst_idx) {
+        const int *__restrict__ dyn_hi_ptr, const int *__restrict__ dst_idx,
+        int *__restrict__ init_status) {
+    // a one-stream pass's status words start here (k_pass_init's duty, one
+    // kernel and one boundary fewer; nothing before the commit reads them)
+    if (init_status && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2 * STATUS_INTS)
+        init_status[threadIdx.x] = threadIdx.x == 0 ? -1 : 0;
     const int cb = blockIdx.y;  // cluster of a batched launch (dst_cs pods apart)
     keys += (size_t)cb * n_lists * stride;
     bounds += (size_t)cb * n_lists * bstride;
@@ -914,16 +919,17 @@ hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bo
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0, const Dyn *dyn,
                         int dyn_flags, int batch, int64_t dst_cluster_pods,
-                        const int32_t *dst_idx) {
+                        const int32_t *dst_idx, int32_t *init_status) {
     if (dyn) np = dyn->win;
     if (np <= 0) return hipSuccess;
     if (dst_idx && batch != 1) return hipErrorInvalidValue;
+    if (init_status && (dyn || batch != 1)) return hipErrorInvalidValue;
     k_merge<<<dim3((int)(((int64_t)np * MERGE_LANES + MERGE_BLOCK - 1) / MERGE_BLOCK), batch),
               MERGE_BLOCK, 0, st>>>(
         reinterpret_cast<const u64 *>(keys), reinterpret_cast<const u64 *>(bounds), n_lists, stride,
         bstride, src_p0, p0, np, reinterpret_cast<u64 *>(cand_key),
         reinterpret_cast<u64 *>(cand_bound), dst_p0, dyn ? dyn->start : nullptr, dyn ? dyn->hi : 0,
-        dyn_flags, (long long)dst_cluster_pods, dyn ? dyn->hi_ptr : nullptr, dst_idx);
+        dyn_flags, (long long)dst_cluster_pods, dyn ? dyn->hi_ptr : nullptr, dst_idx, init_status);
     return hipGetLastError();
 }
 

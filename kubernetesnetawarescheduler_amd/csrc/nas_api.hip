@@ -666,7 +666,7 @@ PodView main_view(nas_ctx *ctx) {
 // merge across ranks), on stream st behind their cost launch; gbuf picks the
 // gathered-list scratch (one per stream that exchanges)
 int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, int ch,
-                int gbuf, const PodView &v) {
+                int gbuf, const PodView &v, int32_t *init_status = nullptr) {
     const int pr0 = p_lo / nas::COST_BN * nas::COST_BN;
     const int pr1 = (int)nas::round_up(p_hi, nas::COST_BN);
     const int np = pr1 - pr0;
@@ -675,8 +675,9 @@ int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, int
     if (!exchanging(ctx)) {
         HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
                                 n_lists, (int64_t)v.Pp * KC, v.Pp, 0, p_lo, p_hi - p_lo, v.key,
-                                v.bound));
+                                v.bound, 0, nullptr, 0, 1, 0, nullptr, init_status));
     } else {
+        if (init_status) return nas::fail(ctx, NAS_ERR_STATE, "status init rides a local merge only");
         // this rank's lists of pods [pr0, pr1) go straight into one send
         // buffer ([np][8] keys, then [np] bounds), so one all-gather moves
         // them; the cross-rank merge reads the rank-major result in place
@@ -2184,7 +2185,9 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         // packet the queue processes between two kernels)
         scored[c] = one_stream ? nullptr : tm.mark(ss);
     }
-    if (live_cap) OK(pass_init(sc));
+    // (one stream: the chunk's merge starts the status words itself)
+    const bool init_in_merge = one_stream && live_cap;
+    if (live_cap && !init_in_merge) OK(pass_init(sc));
     // speculative slots: as many as the previous pass of this shape needed
     // (consecutive passes over similar clusters stop alike), enqueued before
     // the first status round trip; a slot whose walk is not halted exits at
@@ -2212,7 +2215,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         // (merging the tail chunk locally before this wait, gated before its
         // exchange / commit, measured within noise at G = 1 and 8:
         // profiles/r04_ab_tail.txt)
-        OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx)));
+        OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx), init_in_merge ? halt : nullptr));
         hipEvent_t c0 = tm.fine(cs);
         // the pass's last commit also writes the status words into the pinned
         // host area when nothing follows it (no speculative slots): the host

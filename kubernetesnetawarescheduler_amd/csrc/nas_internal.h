@@ -280,7 +280,8 @@ hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bo
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,
                         const Dyn *dyn = nullptr, int dyn_flags = 0, int batch = 1,
-                        int64_t dst_cluster_pods = 0, const int32_t *dst_idx = nullptr);
+                        int64_t dst_cluster_pods = 0, const int32_t *dst_idx = nullptr,
+                        int32_t *init_status = nullptr);
 // the commit keeps the working capacity in LDS (and publishes only final
 // values, at the end of each launch) for clusters of up to this many nodes
 bool commit_in_lds(int N);
