@@ -654,48 +654,34 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             int choice = -1;
             unsigned ccost = 0;
             if (!done && COMMIT_BATCH) {
-                // candidate 0 first: most pods take it (3 LDS reads)
-                const u64 k0 = cur.k[0];
-                bool more = k0 != KEY_INVALID && k0 <= cur.bound;
-                if (more) {
-                    const int n = (int)(unsigned)k0;
-                    const int4 v = ld3(n);
-                    if ((int)(cur.r0 <= v.x) & (int)(cur.r1 <= v.y) & (int)(cur.r2 <= v.z)) {
-                        choice = n;
-                        ccost = (unsigned)(k0 >> 32);
-                        more = false;
-                    }
+                // every usable candidate's capacity in one LDS round trip (8
+                // independent reads), the lowest fitting one is the sequential
+                // choice (keys ascend; unusable ones come last).  Candidate 0
+                // first and the other 7 only for the lanes whose first was full
+                // took two round trips: C2 0.467 -> 0.457 ms
+                // (profiles/r04_ab_c2_commit.txt)
+                int4 v[KC];
+#pragma unroll
+                for (int j = 0; j < KC; ++j) {
+                    const u64 k = cur.k[j];
+                    const bool usable = k != KEY_INVALID && k <= cur.bound;
+                    v[j] = ld3(usable ? (int)(unsigned)k : 0);
                 }
-                // the rest at once for the pods whose first candidate is full
-                // (21 independent LDS reads, not up to 7 dependent rounds of
-                // 3): a herd member costs one LDS latency.  Keys ascend and the
-                // unusable ones (> bound, KEY_INVALID) come last, so the lowest
-                // fitting bit is the sequential choice.
-                if (__ballot(more) && more) {
-                    unsigned okm = 0;
-                    int4 v[KC];
+                __builtin_amdgcn_sched_group_barrier(0x100, KC, 0);
+                unsigned okm = 0;
 #pragma unroll
-                    for (int j = 1; j < KC; ++j) {
-                        const u64 k = cur.k[j];
-                        const bool usable = k != KEY_INVALID && k <= cur.bound;
-                        v[j] = ld3(usable ? (int)(unsigned)k : 0);
-                    }
-                    // the 7 reads back to back (hipcc otherwise keeps two in flight)
-                    __builtin_amdgcn_sched_group_barrier(0x100, KC - 1, 0);
-#pragma unroll
-                    for (int j = 1; j < KC; ++j) {
-                        const u64 k = cur.k[j];
-                        const bool usable = k != KEY_INVALID && k <= cur.bound;
-                        okm |= (unsigned)(usable & (cur.r0 <= v[j].x) & (cur.r1 <= v[j].y) &
-                                          (cur.r2 <= v[j].z)) << j;
-                    }
-#pragma unroll
-                    for (int j = KC - 1; j >= 1; --j)  // constant indices (no scratch array)
-                        if ((okm >> j) & 1u) {
-                            choice = (int)(unsigned)cur.k[j];
-                            ccost = (unsigned)(cur.k[j] >> 32);
-                        }
+                for (int j = 0; j < KC; ++j) {
+                    const u64 k = cur.k[j];
+                    const bool usable = k != KEY_INVALID && k <= cur.bound;
+                    okm |= (unsigned)(usable & (cur.r0 <= v[j].x) & (cur.r1 <= v[j].y) & (cur.r2 <= v[j].z))
+                           << j;
                 }
+#pragma unroll
+                for (int j = KC - 1; j >= 0; --j)  // constant indices (no scratch array)
+                    if ((okm >> j) & 1u) {
+                        choice = (int)(unsigned)cur.k[j];
+                        ccost = (unsigned)(cur.k[j] >> 32);
+                    }
             }
             if (!done && !COMMIT_BATCH) {
 #pragma unroll
