@@ -991,8 +991,23 @@ void abort_comms(nas_ctx *ctx) {
 // otherwise block in the collective forever -- and on expiry abort the
 // communicators and poison the context.  (Polling measured equal to the
 // blocking wait on the G = 8 rehearsal: 1.38-1.41 ms per pass either way.)
+// The host waits by polling the event (WAIT_SPIN_MS, then a blocking wait):
+// past its active-wait window the runtime's own wait sleeps on an interrupt,
+// and the wake-up lands on the pass's critical path at its last event (the
+// host unpacks each chunk as it lands, so only the last wait is exposed)
+#ifndef WAIT_SPIN_MS
+#define WAIT_SPIN_MS 20
+#endif
 int wait_event(nas_ctx *ctx, hipEvent_t e) {
     if (!has_coll(ctx) || ctx->opt_comm_timeout_ms <= 0) {
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
+        while (WAIT_SPIN_MS > 0 && clk::now() - t0 < std::chrono::milliseconds(WAIT_SPIN_MS)) {
+            const hipError_t r = hipEventQuery(e);
+            if (r == hipSuccess) return NAS_OK;
+            if (r != hipErrorNotReady) return nas::hip_fail(ctx, r, "hipEventQuery");
+            __builtin_ia32_pause();
+        }
         HIPCK(hipEventSynchronize(e));
         return NAS_OK;
     }
@@ -1019,7 +1034,7 @@ int wait_event(nas_ctx *ctx, hipEvent_t e) {
 
 // stream synchronisation of the calls that may have issued collectives
 int sync_stream(nas_ctx *ctx, hipStream_t st) {
-    if (!has_coll(ctx)) {
+    if (!has_coll(ctx) && WAIT_SPIN_MS <= 0) {
         HIPCK(hipStreamSynchronize(st));
         return NAS_OK;
     }
@@ -1770,8 +1785,7 @@ int nas_reset_capacity(nas_ctx *ctx) {
     if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
     HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)ctx->B * 3 * ctx->cap_n * 4,
                          hipMemcpyDeviceToDevice, ctx->stream));
-    HIPCK(hipStreamSynchronize(ctx->stream));
-    return NAS_OK;
+    return sync_stream(ctx, ctx->stream);
 }
 
 int nas_get_capacity(nas_ctx *ctx, int32_t *cpu_milli, int32_t *mem_kib, int32_t *pods,
