@@ -804,6 +804,9 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, int ch, int32_t *pub,
 }
 
 float decode_cost(uint32_t raw, int dtype);
+void unpack_range(int32_t *__restrict__ node_out, float *__restrict__ cost_out,
+                  int64_t *__restrict__ int_score_out, const int32_t *__restrict__ from,
+                  const int32_t *__restrict__ raw_in, int lo, int hi, int dtype, int &unsched);
 
 int no_batch(nas_ctx *ctx, const char *what) {
     if (ctx->B > 1)
@@ -938,29 +941,12 @@ int place_batch(nas_ctx *ctx, Timer &tm, int32_t *node_out, float *cost_out,
         HIPCK(hipStreamSynchronize(st));
     }
     tm.span(T_TOTAL, t0, t1);
-    std::memcpy(node_out, stage, BP * 4);
-    const uint32_t *raw = reinterpret_cast<const uint32_t *>(stage + BP);
     int unsched = 0, dev_rounds = 0, rounds = 0;
     for (int b = 0; b < B; ++b) {
         dev_rounds += hs[b * nas::STATUS_INTS + 1];
         rounds += hs[b * nas::STATUS_INTS + 2];
     }
-    // branch-free per-pod loops (they vectorise): 320k pods at C5
-    for (size_t i = 0; i < BP; ++i) unsched += node_out[i] < 0;
-    if (cost_out) {
-        if (ctx->dtype == NAS_DT_I8) {
-            for (size_t i = 0; i < BP; ++i)
-                cost_out[i] = node_out[i] < 0 ? 0.f : (float)(int32_t)(raw[i] ^ 0x80000000u);
-        } else {
-            for (size_t i = 0; i < BP; ++i)
-                cost_out[i] = node_out[i] < 0 ? 0.f : decode_cost(raw[i], ctx->dtype);
-        }
-    }
-    if (int_score_out) {
-        const bool i8 = ctx->dtype == NAS_DT_I8;
-        for (size_t i = 0; i < BP; ++i)
-            int_score_out[i] = (node_out[i] < 0 || !i8) ? 0 : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
-    }
+    unpack_range(node_out, cost_out, int_score_out, stage, stage + BP, 0, (int)BP, ctx->dtype, unsched);
     ctx->timings.fit_ms = tm.total(T_FIT);
     ctx->timings.cost_ms = tm.total(T_COST);
     ctx->timings.merge_ms = tm.total(T_MERGE);
@@ -1265,6 +1251,42 @@ int alloc_extended(nas_ctx *ctx) {
         ctx->host_status.bytes = hs_bytes;
     }
     return NAS_OK;
+}
+
+void unpack_range(int32_t *__restrict__ node_out, float *__restrict__ cost_out,
+                  int64_t *__restrict__ int_score_out, const int32_t *__restrict__ from,
+                  const int32_t *__restrict__ raw_in, int lo, int hi, int dtype, int &unsched) {
+    const uint32_t *__restrict__ raw = reinterpret_cast<const uint32_t *>(raw_in);
+    int none = 0;
+    if (dtype == NAS_DT_I8 && cost_out && int_score_out) {
+        // the common case in one pass over the stage (host-memory bound:
+        // 24 B per pod; 0.24 vs 0.49 ms per 100k pods for the per-pod loop
+        // with the dtype test and a possibly aliased counter inside)
+        for (int i = lo; i < hi; ++i) {
+            const int32_t n = from[i];
+            const int32_t v = (int32_t)(raw[i] ^ 0x80000000u);
+            const bool z = n < 0;
+            node_out[i] = n;
+            none += z;
+            cost_out[i] = z ? 0.f : (float)v;
+            int_score_out[i] = z ? 0 : (int64_t)v;
+        }
+        unsched += none;
+        return;
+    }
+    std::memcpy(node_out + lo, from + lo, (size_t)(hi - lo) * 4);
+    for (int i = lo; i < hi; ++i) none += from[i] < 0;
+    unsched += none;
+    if (cost_out)
+        for (int i = lo; i < hi; ++i) cost_out[i] = from[i] < 0 ? 0.f : decode_cost(raw[i], dtype);
+    if (int_score_out) {
+        if (dtype == NAS_DT_I8) {
+            for (int i = lo; i < hi; ++i)
+                int_score_out[i] = from[i] < 0 ? 0 : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
+        } else {
+            std::memset(int_score_out + lo, 0, (size_t)(hi - lo) * 8);
+        }
+    }
 }
 
 float decode_cost(uint32_t raw, int dtype) {
@@ -2275,17 +2297,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     };
     int unsched = 0;
     // decode pods [lo, hi) from a staging area (placements, then raw keys)
+    // (the last chunks land together at the end of the pass, so their unpack
+    // is on the pass's critical path: one tight loop per output with the
+    // dtype hoisted and no aliasing, so each vectorises)
     auto unpack = [&](int lo, int hi, const int32_t *from) {
-        const uint32_t *raw = reinterpret_cast<const uint32_t *>(from + P);
-        std::memcpy(node_out + lo, from + lo, (size_t)(hi - lo) * 4);
-        for (int i = lo; i < hi; ++i) {
-            const bool none = node_out[i] < 0;
-            unsched += none;
-            if (cost_out) cost_out[i] = none ? 0.f : decode_cost(raw[i], ctx->dtype);
-            if (int_score_out)
-                int_score_out[i] = (none || ctx->dtype != NAS_DT_I8)
-                                       ? 0 : (int64_t)(int32_t)(raw[i] ^ 0x80000000u);
-        }
+        unpack_range(node_out, cost_out, int_score_out, from, from + P, lo, hi, ctx->dtype, unsched);
     };
     // the walk's status comes back in one round trip on `st`; meanwhile the
     // host unpacks each chunk as its copy lands.  Values copied behind a commit
