@@ -109,6 +109,13 @@ constexpr int AOS_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 16;
 #ifndef ONE_WAVE_MAX_PODS
 #define ONE_WAVE_MAX_PODS 16384
 #endif
+// cluster batches walk with k_commit (1,024 threads) even when a cluster is
+// short enough for one wave: C5's 64 x 5,000-pod walks 7.93 -> 7.77 ms per
+// pass (profiles/r04_ab_batch_commit.txt); one cluster keeps the one-wave
+// walk below ONE_WAVE_MAX_PODS (C2's herds)
+#ifndef BATCH_ONE_WAVE
+#define BATCH_ONE_WAVE 0
+#endif
 
 // Requests up to this size reserve with one fetch-and-subtract (undone on
 // failure) instead of a compare-and-swap loop: a herd of m pods picking one
@@ -846,7 +853,7 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
-    if (Pp <= ONE_WAVE_MAX_PODS) {
+    if (Pp <= ONE_WAVE_MAX_PODS && (BATCH_ONE_WAVE || batch == 1)) {
         if (COMMIT_AOS && N <= AOS_MAX_NODES) {
             const size_t lds = round_up(16 * (size_t)N, 256) + PF_BYTES;
             static std::atomic<unsigned long long> attr{0};
