@@ -81,7 +81,16 @@ int ensure(nas_ctx *ctx, DevBuf &b, size_t bytes) {
 namespace {
 
 constexpr int RESCORE_PODS = 1024;  // pods per device-side rescore slot (multiple of COST_BN)
-constexpr int GATHER_PODS = 4096;   // dry pods rescored per gathered slot (gathered_slot)
+// dry pods rescored per gathered slot (gathered_slot).  1024, not 4096: a
+// bf16 C3 halt (the last chunk's lists, scored against capacity two chunks
+// stale, run dry in a herd) flags > 4096 pods with STALE_MIN_FIT 2, but the
+// first 1024 of them always let the walk finish -- the slot's cost launch
+// 690 -> 235 us, the halting pass's slots 0.9 -> 0.37 ms (traced); 256 / 512
+// need more slots (profiles/r04_ab_gather_pods.txt)
+#ifndef GATHER_PODS_MAX
+#define GATHER_PODS_MAX 1024
+#endif
+constexpr int GATHER_PODS = GATHER_PODS_MAX;
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
 constexpr int MAX_SPEC_SLOTS = 8;         // speculative slots at most (nas_place, slot_hint)
 // ... except the second check: a walk still halted after a full batch is
