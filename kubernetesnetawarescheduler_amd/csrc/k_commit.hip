@@ -365,7 +365,13 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     __syncthreads();  // every thread has read the halt word
     if (tid == 0 && h >= 0) {
         halt[0] = -1;
-        if (resume) halt[1] += 1;  // device-side rescores, reported in nas_timings
+        // device-side rescores, reported in nas_timings; the first resume's
+        // pod (the pass's first halt) tells the host which pods' copies were
+        // final before it
+        if (resume) {
+            if (halt[1] == 0) halt[3] = h;
+            halt[1] += 1;
+        }
     }
     int round = 0;
     int stop = p_end;
@@ -603,7 +609,10 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     Pod cur;
     if (lane == 0 && h >= 0) {
         halt[0] = -1;
-        if (resume) halt[1] += 1;
+        if (resume) {
+            if (halt[1] == 0) halt[3] = h;
+            halt[1] += 1;
+        }
     }
     unsigned char *pf = reinterpret_cast<unsigned char *>(smem) +
                         (AOS ? (16 * N + 255) / 256 * 256 : LDS_CAP ? (3 * N * 4 + 255) / 256 * 256 : 0);
