@@ -236,7 +236,8 @@ int nas_upload_latency(nas_ctx *ctx, const void *L, int32_t dtype, int32_t n);
 int nas_upload_capacity(nas_ctx *ctx, const int32_t *cpu_milli, const int32_t *mem_kib,
                         const int32_t *pods, int32_t n);
 
-/* Reset the working capacity to the last uploaded capacity. */
+/* Reset the working capacity to the last uploaded capacity.  Stream-ordered:
+ * returns without waiting; every later call on this context sees the reset. */
 int nas_reset_capacity(nas_ctx *ctx);
 
 /* Read back the working (remaining) capacity. */

@@ -1814,9 +1814,14 @@ int nas_reset_capacity(nas_ctx *ctx) {
     NAS_RANGE("nas_reset_capacity");
     OK(bind(ctx));
     if (!ctx->have_cap) return nas::fail(ctx, NAS_ERR_STATE, "no capacity uploaded");
+    // stream-ordered, no host wait: every later entry point's device work runs
+    // on ctx->stream or behind an event recorded on it (nas_place's other
+    // streams start behind `ready`), and every host read of the capacity syncs
+    // ctx->stream -- the round trip here cost each reset-then-place cycle a
+    // launch + wait (~30-50 us; C2's whole pass is ~450 us)
     HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)ctx->B * 3 * ctx->cap_n * 4,
                          hipMemcpyDeviceToDevice, ctx->stream));
-    return sync_stream(ctx, ctx->stream);
+    return NAS_OK;
 }
 
 int nas_get_capacity(nas_ctx *ctx, int32_t *cpu_milli, int32_t *mem_kib, int32_t *pods,
