@@ -212,6 +212,29 @@ def test_deterministic_repeat(engine):
     assert (a == b).all() and (ca == cb).all()
 
 
+def test_reset_is_stream_ordered(engine):
+    """nas_reset_capacity returns without waiting: a host read right after it,
+    a place right after it and an upload right after it all see the reset
+    (everything is ordered on the context's stream)."""
+    rng = np.random.default_rng(13)
+    WA, L, free, req = cluster(rng, 1200, 700, cap_scale=0.03)
+    upload(engine, WA, L, free, req, "i8")
+    want = engine.place()[0].copy()
+    for _ in range(3):
+        engine.reset_capacity()
+        assert (engine.get_capacity() == free).all()
+        engine.reset_capacity()
+        got, _, _ = engine.place()
+        assert got.tolist() == want.tolist()
+    # reset, then a new upload at once: the upload wins
+    engine.reset_capacity()
+    engine.upload_capacity(free // 2)
+    assert (engine.get_capacity() == free // 2).all()
+    w2, _, _ = oracle.place(WA, L, req, free // 2, "i8")
+    got, _, _ = engine.place()
+    assert got.tolist() == w2.tolist()
+
+
 def test_synthetic_cluster_sampled(engine):
     """The bench's device-generated cluster (scaled down): candidate lists of
     sampled pods equal the oracle top-4 on the inputs read back from HBM, and
