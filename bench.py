@@ -155,7 +155,11 @@ class Dist:
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            # torchrun's env:// store by default; NAS_DIST_INIT (e.g. a file://
+            # rendezvous, as the CPU tests use) replaces it
+            init = os.environ.get("NAS_DIST_INIT", "env://")
+            dist.init_process_group("gloo", init_method=init, rank=self.rank,
+                                    world_size=self.world)
             self.dist = dist
         # (no GPU: the rank logic alone, as the CPU gloo tests run it)
         self.gpu = torch.cuda.is_available()

@@ -3,8 +3,11 @@ an Engine on cuda:0 holding node shard `rank` of `world` (nas_set_shard),
 candidate lists exchanged over torch.distributed gloo by
 sharded.place_dist_shard.  Run as a child process (never imported by pytest).
 
-  python tests/dist_gpu_worker.py RANK WORLD PORT OUT_PREFIX SEED
+  python tests/dist_gpu_worker.py RANK WORLD INIT_URL OUT_PREFIX SEED
+
+INIT_URL is a file:// rendezvous (no TCP port).
 """
+import datetime
 import os
 import sys
 
@@ -32,11 +35,10 @@ def make_inputs(seed):
 
 
 def main():
-    rank, world, port, out, seed = (int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4],
-                                    int(sys.argv[5]))
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = port
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rank, world, url, out, seed = (int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4],
+                                   int(sys.argv[5]))
+    dist.init_process_group("gloo", init_method=url, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
     WA, L, free, req = make_inputs(seed)
 
     def all_gather(keys, bounds):

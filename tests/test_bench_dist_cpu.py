@@ -3,7 +3,6 @@ Dist (RANK / WORLD_SIZE from the env, barrier, max over ranks, broadcast of
 the RCCL unique id) and time_steps (barrier-bracketed timed region, max over
 ranks) -- what the driver's torchrun launch exercises on the GPU node."""
 import os
-import socket
 import sys
 import time
 
@@ -12,9 +11,9 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, port, out):
-    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2",
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _worker(rank, url, out):
+    # NAS_DIST_INIT: a file rendezvous instead of torchrun's MASTER_PORT
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2", NAS_DIST_INIT=url)
     sys.path.insert(0, ROOT)
     import bench
     d = bench.Dist(2)
@@ -36,10 +35,8 @@ def _worker(rank, port, out):
 
 
 def test_bench_dist_world2(tmp_path):
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    from util import rdv_url
     out = str(tmp_path / "el")
-    mp.spawn(_worker, args=(port, out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(rdv_url(tmp_path), out), nprocs=2, join=True)
     a, b = (float(open(f"{out}.{r}").read()) for r in range(2))
     assert a == b

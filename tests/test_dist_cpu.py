@@ -4,7 +4,6 @@ are all-gathered and merged with the engine's rule, and the merged exact
 prefix must equal the unsharded ranking -- the exchange step nas_place runs
 over RCCL, with torch.distributed gloo standing in for it."""
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -13,7 +12,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
-from util import KEY_INVALID, cluster, keys_from_costs, merge_lists, usable
+from util import KEY_INVALID, cluster, keys_from_costs, merge_lists, rdv_url, usable
 
 P, N, WORLD = 300, 77, 2
 
@@ -28,10 +27,8 @@ def shard_lists(WA, L, req, free, n0, n1, K=8):
     return keys, bound
 
 
-def _worker(rank, port, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+def _worker(rank, url, out):
+    dist.init_process_group("gloo", init_method=url, rank=rank, world_size=WORLD)
     rng = np.random.default_rng(42)  # identical inputs on every rank
     WA, L, free, req = cluster(rng, P, N, cap_scale=0.05)
     n0, n1 = rank * N // WORLD, (rank + 1) * N // WORLD
@@ -51,15 +48,9 @@ def _worker(rank, port, out):
     dist.destroy_process_group()
 
 
-def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def test_sharded_lists_merge_to_global_ranking(tmp_path):
     out = str(tmp_path / "merged")
-    mp.spawn(_worker, args=(free_port(), out), nprocs=WORLD, join=True)
+    mp.spawn(_worker, args=(rdv_url(tmp_path), out), nprocs=WORLD, join=True)
     mk, mb = np.load(out + ".keys.npy"), np.load(out + ".bound.npy")
     rng = np.random.default_rng(42)
     WA, L, free, req = cluster(rng, P, N, cap_scale=0.05)

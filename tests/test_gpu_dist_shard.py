@@ -6,8 +6,6 @@ Both ranks must return the sequential oracle's placements, integer scores and
 remaining capacity -- the exchange logic nas_place runs over RCCL, exercised
 across real process boundaries (RCCL itself refuses two ranks on one GPU)."""
 import os
-import socket
-import subprocess
 import sys
 
 import numpy as np
@@ -19,21 +17,15 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def test_two_process_node_shards_match_oracle(tmp_path):
     sys.path.insert(0, HERE)
     from dist_gpu_worker import make_inputs
+    from util import rdv_url, run_children
     seed, world = 11, 2
     out = str(tmp_path / "shard")
-    port = str(free_port())
-    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_gpu_worker.py"), str(r),
-                               str(world), port, out, str(seed)]) for r in range(world)]
-    rcs = [p.wait(timeout=240) for p in procs]
+    url = rdv_url(tmp_path)  # file rendezvous: no TCP port to collide with
+    rcs = run_children([[sys.executable, os.path.join(HERE, "dist_gpu_worker.py"), str(r),
+                         str(world), url, out, str(seed)] for r in range(world)], timeout=100)
     assert rcs == [0] * world
     res = [np.load(f"{out}.{r}.npz") for r in range(world)]
     WA, L, free, req = make_inputs(seed)

@@ -9,7 +9,6 @@ and tie-heavy snapshots, edge values), and over gloo world_size 2 -- the
 all-gather nas_score_reference runs over RCCL on a node-sharded snapshot."""
 import json
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -18,7 +17,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
-from util import random_snapshot
+from util import random_snapshot, rdv_url
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 FIELDS = ("cpu", "mem", "rx", "tx", "bw", "disk")
@@ -125,10 +124,8 @@ def _inputs():
     return snaps, o1, o2
 
 
-def _worker(rank, port, out):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+def _worker(rank, url, out):
+    dist.init_process_group("gloo", init_method=url, rank=rank, world_size=WORLD)
     snaps, o1, o2 = _inputs()  # identical on every rank; each keeps its slice
     lo, hi = rank * NODES // WORLD, (rank + 1) * NODES // WORLD
     mine = np.array([[v for rec in [oracle.vote_partial(sliced(m, lo, hi), lo, o1[s])]
@@ -145,15 +142,9 @@ def _worker(rank, port, out):
     dist.destroy_process_group()
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def test_gloo_world2_node_sharded_vote(tmp_path):
     out = str(tmp_path / "vote")
-    mp.spawn(_worker, args=(_free_port(), out), nprocs=WORLD, join=True)
+    mp.spawn(_worker, args=(rdv_url(tmp_path), out), nprocs=WORLD, join=True)
     r0, r1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
     assert (r0 == r1).all()  # every rank returns the full result
     snaps, o1, o2 = _inputs()

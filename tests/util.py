@@ -1,9 +1,59 @@
-"""Seeded input generators shared by the CPU and GPU tests."""
+"""Seeded input generators shared by the CPU and GPU tests, and the
+multi-process harness (file-based gloo rendezvous, fail-fast children)."""
 import itertools
+import os
+import subprocess
+import time
 
 import numpy as np
 
 from golden.make_golden import random_snapshot  # noqa: F401  (re-export)
+
+
+def rdv_url(tmp_path):
+    """A gloo rendezvous that needs no TCP port: a probed port can be taken
+    (or held on another address) between the probe and the TCPStore's listen,
+    which is what failed the round-4 driver run with EADDRINUSE.  The file
+    must not exist yet; every rank of one group passes the same URL."""
+    path = os.path.join(str(tmp_path), "rdv")
+    if os.path.exists(path):
+        os.unlink(path)
+    return "file://" + path
+
+
+def run_children(cmds, timeout, env=None, logs=None, cwd=None):
+    """Start one child per command and wait for all of them.  As soon as one
+    exits non-zero, or the deadline passes, every child still running is
+    killed, so a rank that died never leaves its peer waiting in a
+    rendezvous; children are always reaped (no process is left behind).
+    `env` is one mapping for all children or a list of one per child; `logs`
+    optional file paths taking each child's stdout + stderr.
+    Returns the exit codes in command order (negative = killed here)."""
+    envs = env if isinstance(env, list) else [env] * len(cmds)
+    files = [open(f, "w") if f else None for f in (logs or [None] * len(cmds))]
+    procs = [subprocess.Popen(c, env=e, cwd=cwd, stdout=f, stderr=subprocess.STDOUT if f else None)
+             for c, e, f in zip(cmds, envs, files)]
+    rcs = [None] * len(procs)
+    deadline = time.monotonic() + timeout
+    try:
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+            if any(rc not in (None, 0) for rc in rcs) or time.monotonic() > deadline:
+                break
+            time.sleep(0.05)
+    finally:
+        for i, p in enumerate(procs):
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+            if rcs[i] is None:
+                rcs[i] = p.returncode
+        for f in files:
+            if f:
+                f.close()
+    return rcs
 
 
 def stack_snapshots(snaps):
