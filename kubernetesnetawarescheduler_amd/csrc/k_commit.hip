@@ -65,17 +65,8 @@ constexpr int PF_SLOT = 6144;
 constexpr int PF_SLOTS = 4;
 constexpr int PF_BYTES = PF_SLOT * PF_SLOTS;
 constexpr int PF_LOADS = 9;  // LDS-DMA instructions per window
-// build-time knobs (A/B'd on one box): windows in flight beyond
-// the walked one (1..3), the zero-traffic scan, the batched candidate reads
-#ifndef COMMIT_AHEAD
-#define COMMIT_AHEAD 3
-#endif
-#ifndef COMMIT_ZSCAN
-#define COMMIT_ZSCAN 1
-#endif
-#ifndef COMMIT_BATCH
-#define COMMIT_BATCH 1
-#endif
+// windows in flight beyond the walked one (1 vs 3 measured equal)
+constexpr int COMMIT_AHEAD = 3;
 static_assert(COMMIT_AHEAD >= 1 && COMMIT_AHEAD < PF_SLOTS, "ring depth");
 template <int N>
 __device__ __forceinline__ void retire_window();
@@ -83,39 +74,19 @@ __device__ __forceinline__ void retire_window();
 __device__ __forceinline__ void retire_oldest(int younger);
 constexpr int LDS_CAP_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 12;  // + cap_to_lds padding
 constexpr int NO_POD = 0x7fffffff;
-// COMMIT_PROF (diagnostic builds only): k_commit_w prints its shader-clock
-// cycles per phase at the end of every walk
-#ifndef COMMIT_PROF
-#define COMMIT_PROF 0
-#endif
-#if COMMIT_PROF
-#define CPROF_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define CPROF_ADD(acc, a, b) acc += (b) - (a)
-#else
-#define CPROF_T(v)
-#define CPROF_ADD(acc, a, b)
-#endif
 
 // k_commit_w's side-by-side capacity image: 16 B per node beside the ring
 constexpr int AOS_MAX_NODES = (LDS_DYN_MAX - PF_BYTES - 256) / 16;
-#ifndef COMMIT_AOS
-#define COMMIT_AOS 1
-#endif
 // walks of up to this many pods run in one wave (k_commit_w): fewer, exact
 // stops for herds on small clusters (C2: 0.67 -> 0.62 ms per pass; with the
 // zero-traffic scan and no rescore left, 0.55 vs 0.63 ms for k_commit); longer
 // walks keep the 1024-pod windows of k_commit, whose conflict-free rounds
-// commit 16x more pods each (C3: 0.8 vs 2.4 ms of commit per pass)
-#ifndef ONE_WAVE_MAX_PODS
-#define ONE_WAVE_MAX_PODS 16384
-#endif
-// cluster batches walk with k_commit (1,024 threads) even when a cluster is
+// commit 16x more pods each (C3: 0.8 vs 2.4 ms of commit per pass).
+// Cluster batches walk with k_commit (1,024 threads) even when a cluster is
 // short enough for one wave: C5's 64 x 5,000-pod walks 7.93 -> 7.77 ms per
 // pass (profiles/r04_ab_batch_commit.txt); one cluster keeps the one-wave
 // walk below ONE_WAVE_MAX_PODS (C2's herds)
-#ifndef BATCH_ONE_WAVE
-#define BATCH_ONE_WAVE 0
-#endif
+constexpr int ONE_WAVE_MAX_PODS = 16384;
 
 // Requests up to this size reserve with one fetch-and-subtract (undone on
 // failure) instead of a compare-and-swap loop: a herd of m pods picking one
@@ -255,14 +226,10 @@ __device__ __forceinline__ void cap_to_lds(const int *g, int *l, int n3, int wav
 // 100-170 us each for a CU beside the wide cost workgroups and put four more
 // dependent launches into the pass's tail.  Pods past a halt carry stale
 // values here exactly as the copies did; the host re-reads everything then.
-#ifndef STAGE_VEC
-#define STAGE_VEC 1
-#endif
 __device__ __forceinline__ void to_stage(const int *out_node, const unsigned *out_cost,
                                          int *stage_node, unsigned *stage_cost, int p_begin,
                                          int p_end, int t, int nt) {
     if (!stage_node) return;
-#if STAGE_VEC
     // 16-byte stores while both stage arrays are aligned: a quarter of the
     // store instructions over the host link
     auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
@@ -278,7 +245,6 @@ __device__ __forceinline__ void to_stage(const int *out_node, const unsigned *ou
         }
         p_begin += 4 * nv;
     }
-#endif
     for (int i = p_begin + t; i < p_end; i += nt) {
         stage_node[i] = out_node[i];
         if (stage_cost) stage_cost[i] = out_cost[i];
@@ -405,7 +371,7 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             }
             if (done) choice = -1;
             bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
-            if (COMMIT_ZSCAN && rescore && zrow && zrow[i] && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
+            if (rescore && zrow && zrow[i] && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
                 auto ld3 = [&](int n) { return make_int4(ld(n), ld(N + n), ld(2 * N + n), 0); };
                 const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld3, zfrom);
                 if (z != -2) {
@@ -656,20 +622,14 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     take(0, p_begin);
     int round = 0;
     int stop = p_end;
-#if COMMIT_PROF
-    unsigned long long c_pick = 0, c_z = 0, c_resv = 0, c_fin = 0, c_win = 0, c_conf = 0;
-    int n_z = 0, n_zsteps = 0, n_zmax = 0, n_zrounds = 0;
-    CPROF_T(c_start);
-#endif
     for (int base = p_begin, w = 0;; ++w) {
         const int i = base + lane;
         bool done = i >= p_end;
         int zfrom = -1;  // zero-traffic scan resume point (zero_row_scan)
         while (true) {
-            CPROF_T(t0);
             int choice = -1;
             unsigned ccost = 0;
-            if (!done && COMMIT_BATCH) {
+            if (!done) {
                 // every usable candidate's capacity in one LDS round trip (8
                 // independent reads), the lowest fitting one is the sequential
                 // choice (keys ascend; unusable ones come last).  Candidate 0
@@ -699,56 +659,15 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                         ccost = (unsigned)(cur.k[j] >> 32);
                     }
             }
-            if (!done && !COMMIT_BATCH) {
-#pragma unroll
-                for (int j = 0; j < KC; ++j) {
-                    const u64 k = cur.k[j];
-                    if (k == KEY_INVALID || k > cur.bound) break;
-                    const int n = (int)(unsigned)k;
-                    const int4 v = ld3(n);
-                    if (cur.r0 <= v.x && cur.r1 <= v.y && cur.r2 <= v.z) {
-                        choice = n;
-                        ccost = (unsigned)(k >> 32);
-                        break;
-                    }
-                }
-            }
             bool rescore = !done && choice < 0 && cur.bound != KEY_INVALID;
-            CPROF_T(t1);
-            CPROF_ADD(c_pick, t0, t1);
-#if COMMIT_PROF
-            n_z += __builtin_popcountll(__ballot(COMMIT_ZSCAN && rescore && cur.z &&
-                                                 (unsigned)(cur.bound >> 32) == ZERO_COST_KEY));
-#endif
-#if COMMIT_PROF
-            int zs0 = max((int)(unsigned)cur.bound + 1, zfrom);
-#endif
-            if (COMMIT_ZSCAN && rescore && cur.z && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
+            if (rescore && cur.z && (unsigned)(cur.bound >> 32) == ZERO_COST_KEY) {
                 const int z = zero_row_scan<LDS_CAP>(cur.bound, cur.r0, cur.r1, cur.r2, N, ld3, zfrom);
                 if (z != -2) {
                     rescore = false;
                     choice = z;  // -1: nothing fits (NAS_EMPTY)
                     ccost = ZERO_COST_KEY;
                 }
-#if COMMIT_PROF
-                zs0 = (zfrom - zs0) / 8 + 1;
-#endif
-            } else {
-#if COMMIT_PROF
-                zs0 = 0;
-#endif
             }
-#if COMMIT_PROF
-            {
-                int mx = zs0;
-                for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-                n_zsteps += mx;
-                n_zmax = max(n_zmax, mx);
-                n_zrounds += mx > 0;
-            }
-#endif
-            CPROF_T(t2);
-            CPROF_ADD(c_z, t1, t2);
             bool g0 = false, g1 = false, g2 = false;
             if (choice >= 0)
                 reserve3<LDS_CAP>(cap + ci(0, choice), cap + ci(1, choice), cap + ci(2, choice), cur.r0,
@@ -756,16 +675,12 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
             const bool bad = rescore || (choice >= 0 && !(g0 && g1 && g2));
             const u64 bm = __ballot(bad);
             ++round;
-            CPROF_T(t3);
-            CPROF_ADD(c_resv, t2, t3);
             if (bm == 0) {  // no conflict: every pending pod of the window commits
                 if (!done) {
                     out_node[i] = choice >= 0 ? choice : NAS_EMPTY;
                     out_cost[i] = ccost;
                     publish(choice, cur);
                 }
-                CPROF_T(t4);
-                CPROF_ADD(c_fin, t3, t4);
                 break;
             }
             const int sl = (int)__builtin_ctzll(bm);
@@ -800,11 +715,8 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
                     done = true;
                 }
             }
-            CPROF_T(t5);
-            CPROF_ADD(c_conf, t3, t5);
         }
         if (stop < p_end || base + 64 >= p_end) break;
-        CPROF_T(tw0);
         // window w+1 (slot (w+1) % 4): windows w+2, w+3 may stay in flight
         younger = 0;
         for (int j = 2; j <= COMMIT_AHEAD; ++j) younger += base + 64 * j < p_end;
@@ -813,18 +725,8 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
         base += 64;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot w % 4's reads done
         issue(base + 64 * COMMIT_AHEAD, (w + 1 + COMMIT_AHEAD) & 3);  // window w+1+AHEAD
-        CPROF_T(tw1);
-        CPROF_ADD(c_win, tw0, tw1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no untracked load outlives the walk
-#if COMMIT_PROF
-    CPROF_T(c_end);
-    if (lane == 0)
-        printf("CPROF pods=%d rounds=%d zpods=%d zsteps=%d zmax=%d zrounds=%d total=%llu pick=%llu "
-               "zscan=%llu reserve=%llu commit_fast=%llu conflict=%llu window=%llu\n", p_end - p_begin,
-               round, n_z, n_zsteps, n_zmax, n_zrounds, c_end - c_start, c_pick, c_z, c_resv, c_fin,
-               c_conf, c_win);
-#endif
     if (lane == 0) {
         if (stop < p_end) *halt = stop;
         halt[2] += round;
@@ -862,8 +764,8 @@ hipError_t launch_commit(hipStream_t st, const uint64_t *cand_key, const uint64_
     const auto *ck = reinterpret_cast<const u64 *>(cand_key);
     const auto *cb = reinterpret_cast<const u64 *>(cand_bound);
     auto *oc = reinterpret_cast<unsigned *>(out_cost);
-    if (Pp <= ONE_WAVE_MAX_PODS && (BATCH_ONE_WAVE || batch == 1)) {
-        if (COMMIT_AOS && N <= AOS_MAX_NODES) {
+    if (Pp <= ONE_WAVE_MAX_PODS && batch == 1) {
+        if (N <= AOS_MAX_NODES) {
             const size_t lds = round_up(16 * (size_t)N, 256) + PF_BYTES;
             static std::atomic<unsigned long long> attr{0};
             hipError_t e = set_lds_once(reinterpret_cast<const void *>(&k_commit_w<true, true>),

@@ -39,6 +39,7 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 typedef float v16f __attribute__((ext_vector_type(16)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int BM = COST_BM;   // nodes per tile
@@ -75,6 +76,11 @@ constexpr int WIDE_PODS = 384;
 #ifndef COST_NARROW_SADDR
 #define COST_NARROW_SADDR 1
 #endif
+// MFMA shape: 0 = 32x32 (v_mfma_i32_32x32x32_i8 / _f32_32x32x16_bf16), 1 =
+// 16x16 (v_mfma_i32_16x16x64_i8 / _f32_16x16x32_bf16) at the same wave tile
+#ifndef COST_MFMA16
+#define COST_MFMA16 0
+#endif
 
 template <int DT>
 struct Mma;
@@ -82,8 +88,12 @@ struct Mma;
 template <>
 struct Mma<NAS_DT_I8> {
     using acc_t = v16i;
+    using acc4_t = v4i;
     static __device__ __forceinline__ acc_t mma(v4i a, v4i b, acc_t c) {
         return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ acc4_t mma16(v4i a, v4i b, acc4_t c) {
+        return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
     }
     static __device__ __forceinline__ unsigned okey(int x) { return (unsigned)x ^ 0x80000000u; }
 };
@@ -91,8 +101,13 @@ struct Mma<NAS_DT_I8> {
 template <>
 struct Mma<NAS_DT_BF16> {
     using acc_t = v16f;
+    using acc4_t = v4f;
     static __device__ __forceinline__ acc_t mma(v4i a, v4i b, acc_t c) {
         return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                        __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ acc4_t mma16(v4i a, v4i b, acc4_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                         __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
     }
     static __device__ __forceinline__ unsigned okey(float x) {
@@ -184,12 +199,22 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     constexpr int PPW = PPWB;
     using M = Mma<DT>;
     using acc_t = typename M::acc_t;
+    // accumulator blocks of a wave's 128 nodes x 64 pods: 4 x 2 blocks of
+    // 32 x 32 (16 registers each), or with the 16x16 shape 8 x 4 blocks of
+    // 16 x 16 (4 registers each); the pod is the block's column = the lane
+    // (mod PB), the node its row = register (+ lane group)
+    constexpr bool M16 = COST_MFMA16 != 0;
+    constexpr int AM = M16 ? 8 : 4;
+    constexpr int AN = M16 ? 4 : NI;
+    constexpr int AR = M16 ? 4 : 16;
+    constexpr int PB = M16 ? 16 : 32;  // pods per block
+    using accb_t = std::conditional_t<M16, typename M::acc4_t, acc_t>;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // the fused fit's words after the main loop: behind the cross-wave merge's
     // lists ([NWN][NI][32][9] u64), inside the smallest staging image
     constexpr int FIT_LDS_OFF = 32768;
     static_assert(FIT_LDS_OFF >= NWN * NI * 32 * 9 * 8 &&
-                  FIT_LDS_OFF + NW * NI * 2 * 64 * 8 <= 2 * STG, "fused-fit LDS words");
+                  FIT_LDS_OFF + NW * AN * 2 * 64 * 8 <= 2 * STG, "fused-fit LDS words");
 
     // ---- XCD-aware tile order: blocks b, b+8, ... share an XCD (speed only)
     const int nwg = n_mt * n_nt;
@@ -333,12 +358,12 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // still holds at the pod's turn) decide every pod that fits all valid
     // nodes or none; the rest compare against the lanes' capacities (three
     // ballots).  The words land where the k_fit mask words would (mwp).
-    int rq[FUSE ? NI : 1][3];
+    int rq[FUSE ? AN : 1][3];
     int fcap[2][3];
     auto fit_issue = [&]() {  // the requests of the lane's pods, its nodes' capacities
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-            const int pod = min(p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31), p_end - 1);
+        for (int ni = 0; ni < AN; ++ni) {
+            const int pod = min(p0 + nt * BNK + wn * WPODS + ni * PB + (lane & (PB - 1)), p_end - 1);
 #pragma unroll
             for (int r = 0; r < 3; ++r) rq[ni][r] = fs.req[(size_t)r * Pp + pod];
         }
@@ -358,7 +383,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // per pod group in the epilogue (held in registers beside the 128
     // accumulators they spilled: 24 B of scratch per lane)
     auto fit_slot = [&](int ni, int mi2) -> u64 * {
-        return reinterpret_cast<u64 *>(lds + FIT_LDS_OFF) + ((w * NI + ni) * 2 + mi2) * 64 + lane;
+        return reinterpret_cast<u64 *>(lds + FIT_LDS_OFF) + ((w * AN + ni) * 2 + mi2) * 64 + lane;
     };
     auto fit_words = [&]() {
 #pragma unroll
@@ -378,13 +403,14 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                 mx[r] = __builtin_amdgcn_readfirstlane(x);
             }
 #pragma unroll
-            for (int ni = 0; ni < NI; ++ni) {
+            for (int ni = 0; ni < AN; ++ni) {
                 const int a = rq[ni][0], bq = rq[ni][1], d = rq[ni][2];
                 const bool all = a <= mn[0] && bq <= mn[1] && d <= mn[2];
                 const bool none = a > mx[0] || bq > mx[1] || d > mx[2];
                 u64 word = all ? valid : 0ull;
-                // lanes l and l + 32 hold the same pod: decide lanes 0..31
-                u64 rest = __builtin_amdgcn_ballot_w64(!all && !none) & 0xffffffffull;
+                // lanes l and l + PB (+ 2 PB, 3 PB) hold the same pod: decide
+                // lanes 0..PB-1
+                u64 rest = __builtin_amdgcn_ballot_w64(!all && !none) & ((1ull << PB) - 1);
                 while (rest) {
                     const int i = (int)__builtin_ctzll(rest);
                     rest &= rest - 1;
@@ -393,7 +419,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                     const u64 m = __builtin_amdgcn_ballot_w64(ra <= fcap[mi2][0]) &
                                   __builtin_amdgcn_ballot_w64(rb <= fcap[mi2][1]) &
                                   __builtin_amdgcn_ballot_w64(rd <= fcap[mi2][2]);
-                    if ((lane & 31) == i) word = m;
+                    if ((lane & (PB - 1)) == i) word = m;
                 }
                 *fit_slot(ni, mi2) = word;
             }
@@ -404,25 +430,26 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // under the main loop (k_fit wrote them before this launch)
     // (issued after the overflow seeding, whose loop they would otherwise
     // stay live across)
-    u64 mwp[NI][2];
+    u64 mwp[AN][2];
     auto load_mask = [&]() __attribute__((always_inline)) {
         if constexpr (!FUSE) {
 #pragma unroll
-            for (int ni = 0; ni < NI; ++ni)
+            for (int ni = 0; ni < AN; ++ni)
 #pragma unroll
                 for (int mi2 = 0; mi2 < 2; ++mi2) {
-                    const int pod = min(p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31), p_end - 1);
+                    const int pod = min(p0 + nt * BNK + wn * WPODS + ni * PB + (lane & (PB - 1)), p_end - 1);
                     const int chunk = (mt * BM + wm * 128 + mi2 * 64) >> 6;
                     mwp[ni][mi2] = mask[(size_t)chunk * Pp + pod];
                 }
         }
     };
-    acc_t acc[4][NI];
+    accb_t acc[AM][AN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < AM; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = acc_t{};
-    int fr = lane & 31, fh = lane >> 5;
+        for (int j = 0; j < AN; ++j) acc[i][j] = accb_t{};
+    // fr: the lane's pod within a block; fh: its row group (rows 4 fh ..)
+    int fr = lane & (PB - 1), fh = lane / PB;
     // ---- exact int32 traffic: the entries outside the int8 plane (nas::Ovf):
     // e * L[m][n] for the lane's 64 nodes per pod are the accumulators'
     // initial value (4 dwords of Lr per 32-node tile: rows (reg & 3) +
@@ -444,8 +471,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
             const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
 #pragma unroll
-            for (int ni = 0; ni < NI; ++ni) {
-                const int r = p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31);
+            for (int ni = 0; ni < AN; ++ni) {
+                const int r = p0 + nt * BNK + wn * WPODS + ni * PB + fr;
                 int beg = 0, end = 0;
                 if (r < cnt_lim && r < p_end) {
                     const int pod = (ov.row_pod ? ov.row_pod[r] : r) + cb * Pp;
@@ -453,12 +480,12 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                     end = ov.ptr[pod + 1];
                 }
 #pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
+                for (int mi = 0; mi < AM; ++mi)
                     for (int j = beg; j < end; ++j) {
                         const int e = ov.e[j];
-                        const signed char *row = lr + (size_t)ov.m[j] * (n_mt * BM) + mi * 32;
+                        const signed char *row = lr + (size_t)ov.m[j] * (n_mt * BM) + mi * (128 / AM);
 #pragma unroll
-                        for (int g = 0; g < 4; ++g) {
+                        for (int g = 0; g < AR / 4; ++g) {
                             const int v = *reinterpret_cast<const int *>(row + 8 * g);
 #pragma unroll
                             for (int c = 0; c < 4; ++c)
@@ -475,7 +502,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                 const signed char *lr = ov.Lr + (size_t)cb * ov.N * (n_mt * BM) + mt * BM + wm * 128 + 4 * fh;
                 // pod group ni's entries [beg, end)
                 auto bounds = [&](int ni, int &beg, int &end) {
-                    const int r = p0 + nt * BNK + wn * WPODS + ni * 32 + (lane & 31);
+                    const int r = p0 + nt * BNK + wn * WPODS + ni * PB + fr;
                     beg = end = 0;
                     if (r < cnt_lim && r < p_end) {
                         const int pod = (ov.row_pod ? ov.row_pod[r] : r) + cb * Pp;
@@ -484,24 +511,24 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                     }
                 };
                 {
-                    int beg[NI], end[NI];
+                    int beg[AN], end[AN];
 #pragma unroll
-                    for (int ni = 0; ni < NI; ++ni) bounds(ni, beg[ni], end[ni]);
+                    for (int ni = 0; ni < AN; ++ni) bounds(ni, beg[ni], end[ni]);
 #pragma unroll
-                    for (int ni = 0; ni < NI; ++ni)
+                    for (int ni = 0; ni < AN; ++ni)
                         for (int j = beg[ni]; j < end[ni]; ++j) {
                             const int e = ov.e[j];
                             const signed char *row = lr + (size_t)ov.m[j] * (n_mt * BM);
-                            int v[4][4];
+                            int v[AM][AR / 4];
 #pragma unroll
-                            for (int mi = 0; mi < 4; ++mi)
+                            for (int mi = 0; mi < AM; ++mi)
 #pragma unroll
-                                for (int g = 0; g < 4; ++g)
-                                    v[mi][g] = *reinterpret_cast<const int *>(row + mi * 32 + 8 * g);
+                                for (int g = 0; g < AR / 4; ++g)
+                                    v[mi][g] = *reinterpret_cast<const int *>(row + mi * (128 / AM) + 8 * g);
 #pragma unroll
-                            for (int mi = 0; mi < 4; ++mi)
+                            for (int mi = 0; mi < AM; ++mi)
 #pragma unroll
-                                for (int g = 0; g < 4; ++g)
+                                for (int g = 0; g < AR / 4; ++g)
 #pragma unroll
                                     for (int c = 0; c < 4; ++c)
                                         acc[mi][ni][4 * g + c] += e * (int)(signed char)(v[mi][g] >> (8 * c));
@@ -517,6 +544,33 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     auto compute = [&](int buf) {
         const unsigned char *As = abuf(buf);
         const unsigned char *Bs = bbuf(buf);
+        if constexpr (M16) {
+            // 16x16x64 (i8) / 16x16x32 (bf16): a fragment is 16 rows x 64 B of
+            // K, lane l holding row l & 15, bytes 16 (l >> 4) .. +16 of the
+            // substep's 64 (the same map on both operands, so the product
+            // sums every k once); chunk 4 kk + fh swizzled by (row >> 1) & 7,
+            // i.e. ((fh ^ s) << 4) ^ (kk << 6) past the row base: conflict-free
+            // ds_read_b128 in its 16-lane groups (rows 0-3/12-15 of one chunk
+            // with rows 4-11 of the next)
+            const unsigned sw = (unsigned)((fh ^ ((fr >> 1) & 7)) << 4);
+            const unsigned ao0 = (unsigned)((wm * 128 + fr) * BKB) + sw;
+            const unsigned bo0 = (unsigned)((wn * WPODS + fr) * BKB) + sw;
+#pragma unroll
+            for (int kk = 0; kk < BKB / 64; ++kk) {
+                const unsigned ao = ao0 ^ (unsigned)(kk << 6), bo = bo0 ^ (unsigned)(kk << 6);
+                v4i bq[AN];
+#pragma unroll
+                for (int ni = 0; ni < AN; ++ni)
+                    bq[ni] = *reinterpret_cast<const v4i *>(Bs + bo + ni * 16 * BKB);
+#pragma unroll
+                for (int mi = 0; mi < AM; ++mi) {
+                    const v4i aq = *reinterpret_cast<const v4i *>(As + ao + mi * 16 * BKB);
+#pragma unroll
+                    for (int ni = 0; ni < AN; ++ni) acc[mi][ni] = M::mma16(aq, bq[ni], acc[mi][ni]);
+                }
+            }
+            return;
+        } else {
         v4i a[2][4], bb[2][NI];
         // fragment (kk, mi) of row r = base + mi * 32 + fr sits at r * BKB +
         // ((2 kk + fh) ^ ((r >> 1) & 7)) * 16 = (row0 * BKB + ((fh ^ s) << 4)) ^
@@ -557,6 +611,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                 for (int ni = 0; ni < NI; ++ni)
                     acc[mi][ni] = M::mma(a[kk & 1][mi], bb[kk & 1][ni], acc[mi][ni]);
         }
+        }
     };
 
     // two-stage pipeline: stage t+1 streams in (LDS-DMA) while t is read
@@ -584,8 +639,8 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         int l;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
         lane = l;
-        fr = l & 31;
-        fh = l >> 5;
+        fr = l & (PB - 1);
+        fh = l / PB;
     }
     if constexpr (FUSE) {
         // the fused fit, after the main loop: nothing of it is live across
@@ -596,28 +651,35 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         fit_words();
     }
     // ---- epilogue: fit mask + per-pod candidate list
-    // per lane: top-4 of its 64 (node, cost) values per pod; lanes l and l^32
-    // (same pod, complementary rows) merge into a sorted 8-list whose bound is
-    // the smaller of the two 4th keys (every key <= bound is in the list)
-    u64 key[NI][8], bnd[NI];
+    // per lane: top-4 of its 64 (32 with the 16x16 shape) (node, cost) values
+    // per pod; the lanes holding the same pod (complementary rows: l, l^32;
+    // 16x16: l, l^16, l^32, l^48) merge into a sorted 8-list whose bound is
+    // the smallest of the 4th keys (every key <= bound is in the list)
+    // value (mi, reg) of the lane: node offset within the wave's 128 (in
+    // increasing order of the slot mi * AR + reg), and its fit bit = that
+    // offset's bit of fit word off >> 6
+    auto noff = [&](int mi, int reg) -> int {
+        return M16 ? mi * 16 + 4 * fh + reg : mi * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * fh;
+    };
+    u64 key[AN][8], bnd[AN];
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
+    for (int ni = 0; ni < AN; ++ni) {
         u64 mwf[2];
         if constexpr (FUSE) {
 #pragma unroll
             for (int mi2 = 0; mi2 < 2; ++mi2) mwf[mi2] = *fit_slot(ni, mi2);
         }
         const u64 *mw = FUSE ? mwf : mwp[ni];
-        // orderable keys of the lane's 64 (node, cost) values and their range
+        // orderable keys of the lane's (node, cost) values and their range
         // (int8: the range of the raw int32 costs -- the key is x ^ 2^31, so
         // key differences are cost differences)
-        unsigned u[4][16];
+        unsigned u[AM][AR];
         unsigned kmin = 0xffffffffu, kmax = 0u;
         int smin = 0x7fffffff, smax = -0x7fffffff - 1;
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi)
+        for (int mi = 0; mi < AM; ++mi)
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
+            for (int reg = 0; reg < AR; ++reg) {
                 if constexpr (DT == NAS_DT_I8) {
                     smin = min(smin, (int)acc[mi][ni][reg]);
                     smax = max(smax, (int)acc[mi][ni][reg]);
@@ -631,10 +693,20 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             kmin = M::okey(smin);
             kmax = M::okey(smax);
         }
+        // the lane's fit bits of block mi, bit (M16: reg; else row(reg)) of a
+        // 32-bit word: M16 the lane's nibble, else the block's 32-node half
+        auto block_bits = [&](int mi) -> unsigned {
+            if constexpr (M16)
+                return (unsigned)(mw[mi >> 2] >> ((mi & 3) * 16 + 4 * fh)) & 0xfu;
+            else
+                return (unsigned)(mw[mi >> 1] >> (32 * (mi & 1)));
+        };
+        constexpr unsigned ALL_BITS = M16 ? 0xfu : 0xffffffffu;
+        auto bitpos = [&](int reg) -> int { return M16 ? reg : (reg & 3) + 8 * (reg >> 2) + 4 * fh; };
         u64 k4[4];
         if (__all(kmax - kmin < (1u << 26) - 1u)) {
             // packed path (every lane's keys span < 2^26 - 1): one u32 per
-            // value, (key - kmin) << 6 | i with i = mi*16 + reg increasing in
+            // value, (key - kmin) << 6 | i with i = mi*AR + reg increasing in
             // node order, so u32 order = (cost, node) order; a non-fitting
             // value is all-ones (never < a fitting one, < 2^32 - 1).  Sorted
             // insert of x into c0 <= .. <= c3: c3 = med3(c2, c3, x), c2 =
@@ -645,7 +717,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             // (key base = okey(0)); otherwise relative to the lane's base
             // (int8: raw = cost bits, base = min cost; bf16: raw = key, base =
             // kmin).  Epilogue VALU per value 8 -> 5 (direct, every node of the
-            // 32-node half fitting every lane's pod: one v_lshl_or_b32) / 7
+            // block fitting every lane's pod: one v_lshl_or_b32) / 7
             // (PMC: the epilogue is VALU-issue-bound, 1,377 instructions per
             // wave = ~10% of a C5 launch, profiles/r03_pmc_epilogue.txt)
             const bool direct = DT == NAS_DT_I8 && __all(smin >= 0 && smax < (1 << 26) - 1);
@@ -658,63 +730,60 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
                 c0 = min(c0, x);
             };
 #pragma unroll
-            for (int mi2 = 0; mi2 < 2; ++mi2)
+            for (int mi = 0; mi < AM; ++mi) {
+                const unsigned bitsw = block_bits(mi);
+                const unsigned nbits = ~bitsw;
+                if (direct && __all(bitsw == ALL_BITS)) {
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int mi = mi2 * 2 + h;
-                    const unsigned bitsw = (unsigned)(mw[mi2] >> (32 * h));
-                    const unsigned nbits = ~bitsw;
-                    if (direct && __all(bitsw == 0xffffffffu)) {
+                    for (int reg = 0; reg < AR; ++reg)
+                        insert(((unsigned)(int)acc[mi][ni][reg] << 6) | (unsigned)(mi * AR + reg));
+                } else {
 #pragma unroll
-                        for (int reg = 0; reg < 16; ++reg)
-                            insert(((unsigned)(int)acc[mi][ni][reg] << 6) | (unsigned)(mi * 16 + reg));
-                    } else {
-#pragma unroll
-                        for (int reg = 0; reg < 16; ++reg) {
-                            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
-                            const unsigned raw = DT == NAS_DT_I8 ? (unsigned)(int)acc[mi][ni][reg]
-                                                                 : u[mi][reg];
-                            // (raw << 6) - (base << 6) in one v_lshl_add (hipcc
-                            // otherwise emits a subtract and a shift); slot and
-                            // the sign-extended not-fit bit (v_bfe_i32) OR'ed in
-                            unsigned y;
-                            if (direct) {
-                                y = raw << 6;
-                            } else {
-                                asm("v_lshl_add_u32 %0, %1, 6, %2" : "=v"(y) : "v"(raw), "v"(nk6));
-                            }
-                            insert(y | (unsigned)(mi * 16 + reg) |
-                                   (unsigned)__builtin_amdgcn_sbfe((int)nbits, row, 1));
+                    for (int reg = 0; reg < AR; ++reg) {
+                        const unsigned raw = DT == NAS_DT_I8 ? (unsigned)(int)acc[mi][ni][reg]
+                                                             : u[mi][reg];
+                        // (raw << 6) - (base << 6) in one v_lshl_add (hipcc
+                        // otherwise emits a subtract and a shift); slot and
+                        // the sign-extended not-fit bit (v_bfe_i32) OR'ed in
+                        unsigned y;
+                        if (direct) {
+                            y = raw << 6;
+                        } else {
+                            asm("v_lshl_add_u32 %0, %1, 6, %2" : "=v"(y) : "v"(raw), "v"(nk6));
                         }
+                        insert(y | (unsigned)(mi * AR + reg) |
+                               (unsigned)__builtin_amdgcn_sbfe((int)nbits, bitpos(reg), 1));
                     }
                 }
+            }
             const unsigned cc[4] = {c0, c1, c2, c3};
             const unsigned nb = (unsigned)(node_base + mt * BM + wm * 128 + 4 * fh);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const unsigned i = cc[j] & 63u, r = i & 15u;
-                const unsigned node = nb + (i >> 4) * 32u + (r & 3u) + 8u * (r >> 2);
+                const unsigned i = cc[j] & 63u;
+                unsigned node;
+                if constexpr (M16) {
+                    node = nb + (i >> 2) * 16u + (i & 3u);
+                } else {
+                    const unsigned r = i & 15u;
+                    node = nb + (i >> 4) * 32u + (r & 3u) + 8u * (r >> 2);
+                }
                 k4[j] = cc[j] == 0xffffffffu ? KEY_INVALID
                                              : ((u64)((cc[j] >> 6) + kbase) << 32) | node;
             }
         } else {
             Top4 t4;
             t4.init();
+            const unsigned node0 = (unsigned)(node_base + mt * BM + wm * 128);
 #pragma unroll
-            for (int mi2 = 0; mi2 < 2; ++mi2) {
+            for (int mi = 0; mi < AM; ++mi) {
+                const unsigned bits = block_bits(mi);
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int mi = mi2 * 2 + h;
-                    const unsigned bits = (unsigned)(mw[mi2] >> (32 * h));
-                    const unsigned node0 = (unsigned)(node_base + mt * BM + wm * 128 + mi * 32);
-#pragma unroll
-                    for (int reg = 0; reg < 16; ++reg) {
-                        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * fh;
-                        // not fitting -> cost all-ones, never inserted (branch-free)
-                        const unsigned key = DT == NAS_DT_I8 ? M::okey(acc[mi][ni][reg]) : u[mi][reg];
-                        const unsigned x = key | ((((bits >> row) & 1u) ^ 1u) * 0xffffffffu);
-                        t4.insert(x, node0 + row);
-                    }
+                for (int reg = 0; reg < AR; ++reg) {
+                    // not fitting -> cost all-ones, never inserted (branch-free)
+                    const unsigned key = DT == NAS_DT_I8 ? M::okey(acc[mi][ni][reg]) : u[mi][reg];
+                    const unsigned x = key | ((((bits >> bitpos(reg)) & 1u) ^ 1u) * 0xffffffffu);
+                    t4.insert(x, node0 + noff(mi, reg));
                 }
             }
 #pragma unroll
@@ -722,13 +791,51 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         }
         u64 o4[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o4[j] = shfl_xor64(k4[j], 32);
+        for (int j = 0; j < 4; ++j) o4[j] = shfl_xor64(k4[j], M16 ? 16 : 32);
         merge44(k4, o4, key[ni]);
         bnd[ni] = umin64(k4[3], o4[3]);
+        if constexpr (M16) {  // the other two row groups (lanes l ^ 32)
+            u64 o8[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o8[j] = shfl_xor64(key[ni][j], 32);
+            const u64 ob = shfl_xor64(bnd[ni], 32);
+            merge88(key[ni], o8);
+            bnd[ni] = umin64(umin64(bnd[ni], ob), key[ni][7]);
+        }
     }
 
     // merge the two node-half waves (wm = 0, 1) through LDS
-    u64 *xk = reinterpret_cast<u64 *>(lds);  // [wn][ni][32][9], staging is dead
+    u64 *xk = reinterpret_cast<u64 *>(lds);  // [wn][64 pods][9], staging is dead
+    if constexpr (M16) {
+        // every lane holds all four pod blocks' lists; lane l takes pod l of
+        // the wave (block fh, pod fr): selected without a runtime index
+        // (which would put the lists in scratch)
+        u64 mine[8], b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            mine[j] = fh == 0 ? key[0][j] : fh == 1 ? key[1][j] : fh == 2 ? key[2][j] : key[3][j];
+        b = fh == 0 ? bnd[0] : fh == 1 ? bnd[1] : fh == 2 ? bnd[2] : bnd[3];
+        u64 *d = xk + (size_t)(wn * WPODS + lane) * 9;
+        if (wm == 1) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = mine[j];
+            d[8] = b;
+        }
+        __syncthreads();
+        if (wm == 0) {
+            u64 other[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) other[j] = d[j];
+            merge88(mine, other);
+            b = umin64(umin64(b, d[8]), mine[7]);
+            const int pod = p0 + nt * BNK + wn * WPODS + lane;
+            if (pod < p_end) {
+                store8(partial + ((size_t)mt * Pp + pod) * KC, mine);
+                pbound[(size_t)mt * Pp + pod] = b;
+            }
+        }
+        return;
+    } else {
     if (wm == 1 && fh == 0) {
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
@@ -761,6 +868,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             else finish(key[2 * rr + 1], bnd[2 * rr + 1], 2 * rr + 1, rr);
         }
     }
+    }
 }
 
 // merge n_lists candidate lists per pod (list l of pod p at
@@ -776,9 +884,7 @@ constexpr int MERGE_LANES = 8;
 // shard; 1,024-thread blocks do not, and measured 7% slower at G = 8 (the
 // wide tile admits nothing beside it either way: C3 within noise for 256 /
 // 512 / 1,024, profiles/r03_ab_merge_block.txt)
-#ifndef MERGE_BLOCK
-#define MERGE_BLOCK 512
-#endif
+constexpr int MERGE_BLOCK = 512;
 
 __global__ void __launch_bounds__(MERGE_BLOCK)
 k_merge(const u64 *__restrict__ keys, const u64 *__restrict__ bounds, int n_lists,

@@ -29,9 +29,6 @@ constexpr int FIT_THREADS = 256;  // 4 waves = 4 node chunks per block
 constexpr int FIT_WAVES = FIT_THREADS / 64;
 constexpr int FIT_GROUPS_MAX = 8;  // 64-pod groups per block (at most 512 pods)
 constexpr int FIT_PF = 2;          // groups of requests in flight ahead of the one decided
-#ifndef FIT_PAIR
-#define FIT_PAIR 1  // two pods per lane (k_fit2)
-#endif
 
 // G = 64-pod groups per wave (compile time: the group loop is unrolled and the
 // request ring stays in registers).  Measured at the C3 shape (10k nodes x 100k
@@ -267,7 +264,7 @@ hipError_t launch_fit(hipStream_t st, const int32_t *cap, int N, int n0, int nlo
     if (rowmap && batch != 1) return hipErrorInvalidValue;
     if (np <= 0) return hipSuccess;
     const int n_chunks = Mp / 64;
-    if (FIT_PAIR && !rowmap && p0 % 2 == 0) {
+    if (!rowmap && p0 % 2 == 0) {  // two pods per lane (k_fit2)
         // pods per block: up to 512 (4 groups of 128), fewer on small launches
         const int yb2 = (n_chunks + FIT_WAVES - 1) / FIT_WAVES;
         const long long groups2 = ((long long)np + 127) / 128 * yb2;

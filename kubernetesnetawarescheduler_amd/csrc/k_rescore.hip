@@ -29,9 +29,7 @@ constexpr int STALE_THREADS = 256;
 // a pod is flagged when fewer than this many of its usable candidates still
 // fit: the dry ones (0) and those one commit away from running dry, whose
 // lists a herd of neighbours is about to drain
-#ifndef STALE_MIN_FIT
-#define STALE_MIN_FIT 2
-#endif
+constexpr int STALE_MIN_FIT = 2;
 
 // One launch: every block flags its pods (ballot words), and the LAST block
 // to finish (ticket counter ctl[3], zeroed at the start of every pass and

@@ -87,10 +87,7 @@ constexpr int RESCORE_PODS = 1024;  // pods per device-side rescore slot (multip
 // first 1024 of them always let the walk finish -- the slot's cost launch
 // 690 -> 235 us, the halting pass's slots 0.9 -> 0.37 ms (traced); 256 / 512
 // need more slots (profiles/r04_ab_gather_pods.txt)
-#ifndef GATHER_PODS_MAX
-#define GATHER_PODS_MAX 1024
-#endif
-constexpr int GATHER_PODS = GATHER_PODS_MAX;
+constexpr int GATHER_PODS = 1024;
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
 constexpr int MAX_SPEC_SLOTS = 8;         // speculative slots at most (nas_place, slot_hint)
 // ... except the second check: a walk still halted after a full batch is
@@ -335,29 +332,22 @@ int prepare_split(nas_ctx *ctx) {
 
 // one cost/top-k launch over the main traffic rows (or a row-mapped view)
 // The wide cost tile (256 nodes x 384 pods, 12 waves) for the main scoring
-// pass of one whole cluster with many pods: the full launch 3.5% (int8) / 6%
-// (bf16) faster, the C3 pass equal (int8) / 9% faster (bf16); on node shards
-// (G = 8 rehearsal: 1.61-1.66 vs 1.42-1.49 ms -- longer workgroups, coarser
-// tails) and on batches of small clusters (C5: 5,000 pods = 13.02 wide tiles)
-// it loses, so those keep the 256 x 256 tile (profiles/r02_s4_ab_wide*.txt)
+// pass of one whole cluster with many pods (full launch 3.5% (int8) / 6%
+// (bf16) faster than 256 x 256: profiles/r02_s4_ab_wide*.txt), for batches of
+// clusters (C5: launch frac 0.42 -> 0.45 although a 5,000-pod cluster is
+// 13.02 wide tiles, profiles/r04_ab_narrow_fit_wide.txt) and for node shards,
+// there together with CU-masked streams (below; the wide tile alone lost on
+// shards in round 2: longer workgroups, coarser tails).  Small clusters,
+// rescore windows and row-mapped views keep 256 x 256.
 constexpr int WIDE_MIN_PODS = 32768;
 // On a node shard (world > 1) the scoring streams leave RESERVE_SHARD_CUS
 // CUs per XCD to the commit stream (set_stream_masks), so the merge /
 // exchange / commit chain runs beside the wide cost tile instead of waiting
 // for one of its workgroups to drain (profiles/r04_ab_reserve.txt)
-#ifndef RESERVE_SHARD_CUS
-#define RESERVE_SHARD_CUS 2  // per XCD; 3 from 8 ranks up (shard_reserve)
-#endif
-#ifndef WIDE_BATCH
-#define WIDE_BATCH 1
-#endif
-#ifndef WIDE_SHARD
-#define WIDE_SHARD 1
-#endif
+constexpr int RESERVE_SHARD_CUS = 2;  // per XCD; 3 from 8 ranks up (shard_reserve)
 bool wide_ok(const nas_ctx *ctx) {
     const bool shard = ctx->world > 1 || ctx->rehearse > 1;
-    if (shard && !WIDE_SHARD) return false;
-    if (ctx->B > 1) return WIDE_BATCH && !shard;
+    if (ctx->B > 1) return !shard;
     return ctx->Pp >= WIDE_MIN_PODS || shard;
 }
 int tile_pods(const nas_ctx *ctx) {
@@ -708,9 +698,6 @@ int merge_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st, int
     return NAS_OK;
 }
 
-#ifndef NAS_FUSE_SHARD
-#define NAS_FUSE_SHARD 0
-#endif
 // scoring for pods [p_lo, p_hi) on stream st against capacity `cap`:
 // fit -> cost/top-k, then (merge = true) merge_range on the same stream over
 // the stream's communicator
@@ -725,13 +712,13 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
     const int np = pr1 - pr0;
     auto *mask = ctx->mask.as<uint64_t>();
     // the cost launch decides the fit itself (fused fit): no k_fit before it.
-    // Not on a node shard (NAS_FUSE_SHARD 0): there the k_fit launch between
-    // two cost launches of a scoring stream is a gap in which the commit
-    // stream's merge / exchange / commit kernels get CUs; with back-to-back
-    // cost launches each of them waited ~100 us for a cost workgroup to
-    // drain (G = 8 rehearsal 1.53 vs 1.34 ms per pass in round 2:
+    // Node shards fuse too since they run the wide tile on CU-masked streams
+    // (round 4): the commit stream's merge / exchange / commit kernels have
+    // CUs of their own, so the k_fit launch between two cost launches is no
+    // longer needed as a gap for them (with the 256 x 256 tile and unmasked
+    // streams each of them had waited ~100 us for a cost workgroup to drain:
     // profiles/r03_g8_timeline_before.txt, r03_ab_fuse_shard.txt)
-    const bool fuse = NAS_FUSE_SHARD || ctx->world == 1 || wide_ok(ctx);
+    const bool fuse = ctx->world == 1 || wide_ok(ctx);
     const nas::FitSrc fit{cap, v.req, ctx->N, ctx->Nloc0, ctx->Nloc};
     hipEvent_t e0 = tm.fine(st);
     if (!fuse)
@@ -990,14 +977,15 @@ void abort_comms(nas_ctx *ctx) {
 // past its active-wait window the runtime's own wait sleeps on an interrupt,
 // and the wake-up lands on the pass's critical path at its last event (the
 // host unpacks each chunk as it lands, so only the last wait is exposed)
-#ifndef WAIT_SPIN_MS
-#define WAIT_SPIN_MS 20
-#endif
+// (each host thread that waits spins on its core for up to WAIT_SPIN_MS:
+// an in-process group of G ranks, one thread each, keeps G cores busy
+// during a pass -- INTEGRATION.md, threading)
+constexpr int WAIT_SPIN_MS = 20;
 int wait_event(nas_ctx *ctx, hipEvent_t e) {
     if (!has_coll(ctx) || ctx->opt_comm_timeout_ms <= 0) {
         using clk = std::chrono::steady_clock;
         const auto t0 = clk::now();
-        while (WAIT_SPIN_MS > 0 && clk::now() - t0 < std::chrono::milliseconds(WAIT_SPIN_MS)) {
+        while (clk::now() - t0 < std::chrono::milliseconds(WAIT_SPIN_MS)) {
             const hipError_t r = hipEventQuery(e);
             if (r == hipSuccess) return NAS_OK;
             if (r != hipErrorNotReady) return nas::hip_fail(ctx, r, "hipEventQuery");
@@ -1027,18 +1015,13 @@ int wait_event(nas_ctx *ctx, hipEvent_t e) {
     }
 }
 
-// stream synchronisation of the calls that may have issued collectives
+// stream synchronisation through wait_event (the spin, and the deadline of
+// calls that may have issued collectives), on the context's own event
+// (created once, destroyed by nas_destroy)
 int sync_stream(nas_ctx *ctx, hipStream_t st) {
-    if (!has_coll(ctx) && WAIT_SPIN_MS <= 0) {
-        HIPCK(hipStreamSynchronize(st));
-        return NAS_OK;
-    }
-    hipEvent_t e = nullptr;
-    HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    hipError_t r = hipEventRecord(e, st);
-    int rc = r == hipSuccess ? wait_event(ctx, e) : nas::hip_fail(ctx, r, "hipEventRecord");
-    (void)hipEventDestroy(e);
-    return rc;
+    if (!ctx->sync_ev) HIPCK(hipEventCreateWithFlags(&ctx->sync_ev, hipEventDisableTiming));
+    const hipError_t r = hipEventRecord(ctx->sync_ev, st);
+    return r == hipSuccess ? wait_event(ctx, ctx->sync_ev) : nas::hip_fail(ctx, r, "hipEventRecord");
 }
 
 // NAS_OPT_INJECT_STALL_MS (tests): delay the stream a call waits on, once,
@@ -1057,11 +1040,10 @@ void inject_stall(nas_ctx *ctx, hipStream_t st) {
 // about 32, so the commit left after the scoring ends (the serial tail, which
 // matters most on a node shard's short scoring) is short.
 constexpr int CHUNK_WORKGROUPS = 512;  // cost workgroups per big chunk (measured best)
-#ifndef CHUNK_TILES_WIDE
-#define CHUNK_TILES_WIDE 48  // 256-pod units per chunk on the wide tile: 32 tiles of 384 (1,280
-                             // workgroups at 40 node tiles, as the 256-pod form's 32-unit chunks);
-                             // 24 / 33 units measured 0.5-2% slower (profiles/r02_s4_ab_chunk.txt)
-#endif
+// 256-pod units per chunk on the wide tile: 32 tiles of 384 (1,280 workgroups
+// at 40 node tiles, as the 256-pod form's 32-unit chunks); 24 / 33 units
+// measured 0.5-2% slower (profiles/r02_s4_ab_chunk.txt)
+constexpr int CHUNK_TILES_WIDE = 48;
 // node tiles per rank for chunk planning: the LARGEST shard's, the same on
 // every rank (rank shards differ by up to one node, so their own Mp can
 // differ by a tile, e.g. 2,049 nodes over 8 ranks: 256 vs 257 nodes); every
@@ -1115,28 +1097,6 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
     return tiles * nas::COST_BN;
 }
 
-#ifndef CHUNK_BALANCE
-#define CHUNK_BALANCE 1
-#endif
-#ifndef SCORE_STREAMS
-#define SCORE_STREAMS 2
-#endif
-// Node shards keep equal chunks: the balanced plan below put two chunk chains
-// in the pass's tail and measured 4-8% slower at G = 8 and 1% at G = 4
-// (profiles/r03_ab_chunk_plan_shard.txt)
-#ifndef CHUNK_BALANCE_SHARD
-#define CHUNK_BALANCE_SHARD 0
-#endif
-#ifndef CHUNK_FIRST_HALF
-#define CHUNK_FIRST_HALF 0
-#endif
-// the pass's last commit writes the status words to the pinned host area
-#ifndef STATUS_IN_COMMIT
-#define STATUS_IN_COMMIT 1
-#endif
-#ifndef CHUNK_MIN_TAIL
-#define CHUNK_MIN_TAIL 0  // 256-pod units: a stream's last chunk at least this long
-#endif
 // The pass's scoring chunks [lo, hi) in pod order; chunk c runs on scoring
 // stream c & 1.  On the wide tile (one cluster, G = 1) the two streams'
 // totals are balanced at the end: the remainder after the 48-unit chunks is
@@ -1146,17 +1106,17 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
 // tiles of 261 at C3, and ran alone -- one partial wave of idle CUs per
 // chunk -- for the last ~1.4 ms of the scoring: profiles/r03_pass_timeline_c3_*.txt,
 // r03_ab_balance_ksweep.txt)
+// Node shards keep equal chunks (chunk_pods mode 2): the balanced plan put
+// two chunk chains in the pass's tail and measured 4-8% slower at G = 8 and
+// 1% at G = 4 (profiles/r03_ab_chunk_plan_shard.txt).  Putting the half-length
+// chunk first (chunks then finish in pod order) measured the same or 0.5%
+// slower, and so did moving units from a stream's short last chunk to its
+// previous one (r03_ab_chunk_order.txt).
 std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
     std::vector<std::pair<int, int>> chunks;
     const int P = ctx->P;
     const bool wide = tile_pods(ctx) != nas::COST_BN && ctx->world == 1;
-    // a node shard with few node tiles: equal chunks of ~CHUNK_WORKGROUPS
-    // cost workgroups (chunk_pods mode 2); balanced the same way only when
-    // built with CHUNK_BALANCE_SHARD=1
-    const int n_mt = plan_n_mt(ctx);
-    const int big_ns = std::max(32, (CHUNK_WORKGROUPS + n_mt - 1) / n_mt);
-    const bool shard = !wide && big_ns > 32 && ctx->B == 1;
-    if (!((CHUNK_BALANCE && wide) || (CHUNK_BALANCE_SHARD && shard))) {
+    if (!wide) {
         for (int c = 0, lo = 0; lo < P; ++c) {
             const int hi = std::min(P, lo + chunk_pods(ctx, c, lo));
             chunks.push_back({lo, hi});
@@ -1174,21 +1134,13 @@ std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
         load[(sizes.size() - 1) & 1] += u;
         left -= u;
     };
-    // wide: 48-unit chunks, the second stream's first one half as long; node
-    // shard: a 32-tile first chunk (the commit stream starts early), then
-    // `big_ns`-tile chunks
-    const int big = wide ? CHUNK_TILES_WIDE : big_ns;
-    // (CHUNK_FIRST_HALF=1 puts the half-length chunk first: chunks then finish
-    // in pod order and the in-order commit chain follows each chunk as it
-    // lands -- one merge + commit chain behind the scoring instead of four --
-    // but the pass measured the same or 0.5% slower: r03_ab_chunk_order.txt)
-    const int first = wide ? (CHUNK_FIRST_HALF ? big / 2 : big) : 32;
-    const int second = wide ? (CHUNK_FIRST_HALF ? big : big / 2) : big;
+    // 48-unit chunks, the second stream's first one half as long
+    const int big = CHUNK_TILES_WIDE;
     if (left <= big) {
         take(left);
     } else {
-        take(first);
-        take(second);
+        take(big);
+        take(big / 2);
         while (left > 0) {
             // can the rest end as one chunk on the next stream s and one on
             // the other, both at most `big`, with equal stream totals?
@@ -1205,19 +1157,6 @@ std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
             }
             take(big);
         }
-    }
-    // (CHUNK_MIN_TAIL > 0: a stream's last chunk shorter than that takes
-    // units from the same stream's previous chunk -- stream totals and pod
-    // order stay.  C3's plan ends in a 3-unit chunk = 80 wide workgroups that
-    // runs nearly alone for one workgroup time, ~190 us,
-    // r03_pass_timeline_c3_final.txt, yet 12 / 18 measured within noise of
-    // it: r03_ab_chunk_order.txt.)
-    for (int i = std::max(2, (int)sizes.size() - 2); i < (int)sizes.size(); ++i) {
-        if (CHUNK_MIN_TAIL <= 0 || sizes[i] >= CHUNK_MIN_TAIL) continue;
-        const int d = (CHUNK_MIN_TAIL - sizes[i] + unit - 1) / unit * unit;
-        if (sizes[i - 2] - d < CHUNK_MIN_TAIL) continue;
-        sizes[i - 2] -= d;
-        sizes[i] += d;
     }
     for (int lo = 0, i = 0; i < (int)sizes.size(); ++i) {
         const int hi = std::min(P, lo + sizes[i] * nas::COST_BN);
@@ -1365,23 +1304,37 @@ struct nas::CommInit {
 };
 
 namespace {
-// join the parked helpers of earlier abandoned inits: the finished ones
-// (wait = false), or all of them (nas_destroy)
-void reap_comm_helpers(nas_ctx *ctx, bool wait) {
-    for (size_t i = 0; i < ctx->comm_helpers.size();) {
-        bool done = wait;
-        if (!wait) {
-            std::lock_guard<std::mutex> g(ctx->comm_helper_state[i]->mu);
-            done = ctx->comm_helper_state[i]->done;
+// join the parked helpers of earlier abandoned inits that have finished;
+// with detach_ms >= 0 (nas_destroy) poll up to that long for the others,
+// then DETACH those still inside RCCL: a helper owns only the shared
+// CommInit record and its own stream, event and buffers (it captures no
+// context pointer), so it may outlive the context, and a helper that never
+// returns from RCCL must not hang the context's teardown
+void reap_comm_helpers(nas_ctx *ctx, int detach_ms = -1) {
+    using clk = std::chrono::steady_clock;
+    const auto until = clk::now() + std::chrono::milliseconds(std::max(detach_ms, 0));
+    for (;;) {
+        for (size_t i = 0; i < ctx->comm_helpers.size();) {
+            bool done;
+            {
+                std::lock_guard<std::mutex> g(ctx->comm_helper_state[i]->mu);
+                done = ctx->comm_helper_state[i]->done;
+            }
+            if (!done) {
+                ++i;
+                continue;
+            }
+            ctx->comm_helpers[i].join();
+            ctx->comm_helpers.erase(ctx->comm_helpers.begin() + i);
+            ctx->comm_helper_state.erase(ctx->comm_helper_state.begin() + i);
         }
-        if (!done) {
-            ++i;
-            continue;
-        }
-        ctx->comm_helpers[i].join();
-        ctx->comm_helpers.erase(ctx->comm_helpers.begin() + i);
-        ctx->comm_helper_state.erase(ctx->comm_helper_state.begin() + i);
+        if (detach_ms < 0 || ctx->comm_helpers.empty()) return;
+        if (clk::now() >= until) break;
+        std::this_thread::sleep_for(std::chrono::milliseconds(10));
     }
+    for (std::thread &t : ctx->comm_helpers) t.detach();
+    ctx->comm_helpers.clear();
+    ctx->comm_helper_state.clear();
 }
 }  // namespace
 
@@ -1439,8 +1392,9 @@ void nas_destroy(nas_ctx *ctx) {
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
     if (ctx->ref_stage.p) (void)hipHostFree(ctx->ref_stage.p);
     destroy_comms(ctx);
-    reap_comm_helpers(ctx, true);
+    reap_comm_helpers(ctx, 2000);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->sync_ev) (void)hipEventDestroy(ctx->sync_ev);
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->stream2);
     (void)hipStreamDestroy(ctx->stream_commit);
@@ -2213,10 +2167,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // above (overflow lists, latency rows, fp32 splits) are read by every
     // chunk's cost launch.
     if (!live_cap) OK(pass_init(st));
-    // the two scoring streams (a CU-masked pair that left 8 or 16 CUs to the
-    // commit stream on node shards measured 25-35% slower at G = 8:
-    // profiles/r03_ab_reserve_cus.txt)
-    const hipStream_t ss2[2] = {st, SCORE_STREAMS == 1 && ctx->world == 1 ? st : ctx->stream2};
+    // the two scoring streams (on a node shard CU-masked by set_stream_masks:
+    // they leave 2-3 CUs per XCD to the commit stream, profiles/r04_ab_reserve.txt;
+    // round 3's masks that reserved 8-16 CUs beside the narrow tile measured
+    // 25-35% slower, r03_ab_reserve_cus.txt)
+    const hipStream_t ss2[2] = {st, ctx->stream2};
     if (!one_stream) {
         hipEvent_t ready = tm.mark(st);
         for (hipStream_t s : {ss2[0], ss2[1], sc})
@@ -2245,7 +2200,8 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     const int spec = (!has_coll(ctx) && ctx->slot_hint_P == P && ctx->slot_hint_N == N) ? ctx->slot_hint : 0;
     // (an injected stall, NAS_OPT_INJECT_STALL_MS, sits on st behind the
     // pass: the host must wait on st then)
-    const bool status_in_commit = STATUS_IN_COMMIT && spec == 0 && ctx->opt_inject_stall_ms == 0;
+    // (the pass's last commit writes the status words to the pinned host area)
+    const bool status_in_commit = spec == 0 && ctx->opt_inject_stall_ms == 0;
     for (size_t c = 0; c < chunks.size(); ++c) {
         const int lo = chunks[c].first, hi = chunks[c].second;
         // the last chunk is merged and committed on its own scoring stream
@@ -2551,7 +2507,7 @@ namespace {
 // 3.96-4.00 / 3.99-4.03, G = 4 2.27-2.29 / 2.19-2.20 / 2.20-2.22 /
 // 2.16-2.20, G = 8 1.28-1.32 / 1.27-1.28 / 1.24-1.26 / 1.24-1.29
 int shard_reserve(int world) {
-    if (world <= 1 || !WIDE_SHARD) return 0;
+    if (world <= 1) return 0;
     return world >= 8 ? RESERVE_SHARD_CUS + 1 : RESERVE_SHARD_CUS;
 }
 // Recreate the context's three streams: reserve > 0 keeps `reserve` CUs of
@@ -2559,7 +2515,12 @@ int shard_reserve(int world) {
 // streams (hipExtStreamCreateWithCUMask: mask bit i is CU i / 8 of XCD i % 8,
 // tools/cumask_probe.hip; an XCD whose bits are all clear would run on ALL its
 // CUs, so every mask keeps CUs on every XCD); reserve 0 restores plain
-// streams.  Only between calls (nothing in flight).
+// streams.  Only between calls (nothing in flight).  The masked streams are
+// BLOCKING streams at the default priority (the CU-mask constructor takes no
+// flags): they serialise with the legacy NULL stream, which nothing of the
+// engine uses (every call works on its own streams and waits on its own
+// events), and the commit stream needs no priority there because it has CUs
+// of its own.
 int set_stream_masks(nas_ctx *ctx, int reserve) {
     if (reserve == ctx->cu_reserve) return NAS_OK;
     int ncu = 0;
@@ -2608,9 +2569,6 @@ int nas_comm_unique_id(uint8_t id_out[128]) {
     return NAS_OK;
 }
 
-#ifndef NAS_COMM_CHILD_BLOCKING
-#define NAS_COMM_CHILD_BLOCKING 0
-#endif
 int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t world) {
     NAS_RANGE("nas_comm_init");
     OK(bind(ctx));
@@ -2623,11 +2581,13 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     destroy_comms(ctx);
     // the previous communicators are gone: until this call succeeds the
     // context is a single rank (a context left at world > 1 without
-    // communicators would fail every sharded call with a null communicator)
+    // communicators would fail every sharded call with a null communicator),
+    // on plain streams (no CUs kept for a commit stream of a shard)
     ctx->rank = 0;
     ctx->world = 1;
     ctx->rehearse = 0;
     ctx->virtual_shard = false;
+    OK(set_stream_masks(ctx, 0));
     int32_t eff_world = world, rehearse = 0;
     if (ctx->opt_rehearse_world > 1 && world == 1) {
         // diagnostic (NAS_OPT_REHEARSE_WORLD): one rank of a G-GPU pass
@@ -2656,9 +2616,14 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
     // it), so no RCCL call of the helper races the main thread's abort; a
     // handle that appears after the claim is aborted by the helper itself.
     // A helper still inside RCCL 30 s after the aborts is parked in the
-    // context (joined by the next nas_comm_init once done, or by
-    // nas_destroy): no thread of this call is ever detached.
-    reap_comm_helpers(ctx, false);
+    // context: joined by the next nas_comm_init once done, or by nas_destroy,
+    // which waits up to 2 s for it and then detaches it (it holds no
+    // reference to the context).  Every communicator is non-blocking
+    // (config.blocking = 0, root and children), so the RCCL calls `guarded`
+    // makes under the mutex (broadcast, warm-up all-gathers, async-error
+    // polls) return at once (ncclInProgress at worst) and never hold the
+    // mutex against the main thread's claim-and-abort.
+    reap_comm_helpers(ctx);
     auto st = std::make_shared<nas::CommInit>();
     const int dev = ctx->device;
     using CI = nas::CommInit;
@@ -2763,7 +2728,7 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
         for (int i = 0; i < 3 && r == ncclSuccess; ++i) {
             what = "ncclCommInitRankConfig (child)";
             ncclConfig_t kc = NCCL_CONFIG_INITIALIZER;
-            kc.blocking = NAS_COMM_CHILD_BLOCKING;
+            kc.blocking = 0;
             r = after_init(i, ncclCommInitRankConfig(&st->kids[i], world, kid_ids[i], rank, &kc));
             if (r == ncclInProgress && load(&st->kids[i])) r = settle(i);
             if (r == ncclSuccess && !load(&st->kids[i])) r = ncclInternalError;
@@ -2863,7 +2828,7 @@ int nas_comm_init(nas_ctx *ctx, const uint8_t id[128], int32_t rank, int32_t wor
                              " ms (NAS_OPT_COMM_TIMEOUT_MS): a rank did not join; "
                              "communicators aborted" +
                              (finished ? "" : " (the helper thread is still inside RCCL: parked in the "
-                                              "context, joined by nas_destroy)"));
+                                              "context, joined later or detached by nas_destroy)"));
     if (st->r != ncclSuccess)
         return nas::fail(ctx, NAS_ERR_COMM, st->what + ": " + ncclGetErrorString(st->r));
     ctx->rank = rank;
@@ -2909,6 +2874,7 @@ int nas_comm_init_local(nas_ctx *ctx, nas_local_group *group, int32_t rank) {
     ctx->world = 1;
     ctx->rehearse = 0;
     ctx->virtual_shard = false;
+    OK(set_stream_masks(ctx, 0));  // (as nas_comm_init: a failed join leaves plain streams)
     {
         std::lock_guard<std::mutex> g(group->g->mu);
         if (group->g->broken) return nas::fail(ctx, NAS_ERR_COMM, "nas_comm_init_local: group is broken");

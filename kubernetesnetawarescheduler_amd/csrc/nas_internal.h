@@ -207,6 +207,7 @@ struct nas_ctx {
     // timing events, created once and reused by every call (hipEventCreate
     // per mark cost a small placement more than its kernels)
     std::vector<hipEvent_t> ev_pool;
+    hipEvent_t sync_ev = nullptr;  // sync_stream's event (created on first use)
     size_t ev_used = 0;
 };
 
