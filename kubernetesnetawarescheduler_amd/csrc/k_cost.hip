@@ -11,9 +11,10 @@
 //
 //  * int8 path: v_mfma_i32_32x32x32_i8, int32 accumulation -- exact, so the
 //    integer scores and the chosen nodes are bit-identical to the oracle.
-//  * bf16 path: v_mfma_f32_32x32x16_bf16, fp32 accumulation; also the fp32
-//    path, whose operands are split into three bf16 planes each and laid out
-//    along a six-fold K (k_misc.hip k_split6: products to 2^-24 relative).
+//  * bf16 path: v_mfma_f32_16x16x32_bf16 (the 16x16 shape: 3.5% faster than
+//    32x32x16 here, see mfma16()), fp32 accumulation; also the fp32 path,
+//    whose operands are split into three bf16 planes each and laid out along
+//    a six-fold K (k_misc.hip k_split6: products to 2^-24 relative).
 //
 // Tile: 256 nodes x 256 pods per 512-thread workgroup (8 wave64 as 2 x 4),
 // each wave 128 nodes x 64 pods = 4 x 2 MFMA 32x32 tiles.  K is staged 128
@@ -24,11 +25,13 @@
 // remapped so the blocks sharing an XCD's L2 cover a 4 (node tiles) x 8
 // (pod tiles) super-tile.
 //
-// Epilogue: per lane, 64 (node, cost) values per pod -> mask from the fit
-// kernel (bit per node) -> sorted top-4 of (orderable cost, node) in
-// registers -> merged with lane^32 into an 8-list with an exactness bound
-// (klist.h) -> merged across the two node-half waves through LDS ->
-// partial[node_tile][pod][8] + pbound[node_tile][pod] (72 B per pod per tile).
+// Epilogue: per lane, 64 (node, cost) values per pod (32 with the 16x16
+// shape) -> mask from the fit kernel (bit per node) -> sorted top-4 of
+// (orderable cost, node) in registers -> merged with the lanes holding the
+// same pod (lane^32; 16x16: lane^16, then lane^32) into an 8-list with an
+// exactness bound (klist.h) -> merged across the two node-half waves through
+// LDS -> partial[node_tile][pod][8] + pbound[node_tile][pod] (72 B per pod
+// per tile).
 #include "klist.h"
 
 #include <type_traits>
@@ -56,10 +59,7 @@ constexpr int BKB = COST_BKB; // bytes of K per LDS stage (full 128-byte lines)
 // variants of this kernel (other pipelines, schedules, one wave per SIMD,
 // cache policies) live in tools/k_cost_diag.hip.
 constexpr int PG_NARROW = 4;
-#ifndef COST_PG_WIDE
-#define COST_PG_WIDE 2
-#endif
-constexpr int PG_WIDE = COST_PG_WIDE;
+constexpr int PG_WIDE = 2;
 // wave layouts: NWN = 4 -> 256 x 256 per 8-wave workgroup (2 node halves x 4
 // pod quarters, each wave 128 nodes x 64 pods = 4 x 2 MFMA 32x32 tiles, 128
 // accumulator registers, two waves per SIMD, 128 KiB LDS double buffer);
@@ -67,21 +67,18 @@ constexpr int PG_WIDE = COST_PG_WIDE;
 // SIMD of the same 128 x 64 shape, 160 KiB LDS double buffer), 17% fewer
 // staged bytes per MAC, for the main scoring pass of one large cluster
 constexpr int WIDE_PODS = 384;
-#ifndef COST_WIDE_SADDR
-#define COST_WIDE_SADDR 1
-#endif
-#ifndef COST_XOR_FRAG
-#define COST_XOR_FRAG 1
-#endif
-#ifndef COST_NARROW_SADDR
-#define COST_NARROW_SADDR 1
-#endif
-// MFMA shape: 0 = 32x32 (v_mfma_i32_32x32x32_i8 / _f32_32x32x16_bf16), 1 =
-// 16x16 (v_mfma_i32_16x16x64_i8 / _f32_16x16x32_bf16) at the same wave tile
-#ifndef COST_MFMA16
-#define COST_MFMA16 0
-#endif
-
+// (8 waves of 128 x 96 per wave for the wide tile -- two per SIMD, 22% fewer
+// LDS fragment reads per MAC -- measured 0.3% slower per C3 launch and 2%
+// per pass in int8, 2.5% slower in bf16, 3-5% slower on C5:
+// profiles/r05b_ab_mfma_shape.txt)
+// MFMA shape per dtype (same box, alternating, profiles/r05b_ab_mfma_shape.txt):
+// bf16 runs v_mfma_f32_16x16x32_bf16 -- the C3 launch 13.40 -> 12.95 ms (0.593
+// -> 0.614 of the bf16 peak): the chip holds a higher clock on the 16x16
+// shape under this power-limited loop (MI355X_MICROARCH.md, DVFS give-back
+// item 7) -- while int8 stays on v_mfma_i32_32x32x32_i8 (16x16x64: launch
+// 6.91 -> 7.26 ms, C5 0.45 -> 0.40)
+template <int DT>
+constexpr bool mfma16() { return DT == NAS_DT_BF16; }
 template <int DT>
 struct Mma;
 
@@ -186,14 +183,15 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
             Ovf ov, const int *__restrict__ rowmap, FitSrc fs) {
     static_assert(NWN == 4 || NWN == 6, "the 8- and 12-wave layouts");
-    static_assert(NWN != 6 || (!RMAP && FUSE), "the wide tile serves the main pass only");
-    static_assert(!FUSE || !RMAP, "the fused fit: main-range launches");
     constexpr int NW = 2 * NWN;              // waves
-    constexpr int NI = 2;                    // 32-pod MFMA tiles per wave
+    constexpr int NI = 2;                    // 32-pod columns per wave
     constexpr int WPODS = 32 * NI;           // pods per wave
     constexpr int BNK = NWN * WPODS;         // pods per tile (256; the wide tile 384)
+    constexpr bool WIDE = BNK > BN;
+    static_assert(!WIDE || (!RMAP && FUSE), "the wide tile serves the main pass only");
+    static_assert(!FUSE || !RMAP, "the fused fit: main-range launches");
     constexpr int STG = (BM + BNK) * BKB;    // bytes per LDS stage
-    constexpr int PG = NWN == 6 ? PG_WIDE : PG_NARROW;
+    constexpr int PG = WIDE ? PG_WIDE : PG_NARROW;
     constexpr int PPWA = (BM / 8 + NW - 1) / NW;   // 1 KiB LDS-DMA pieces of A per wave per stage
     constexpr int PPWB = (BNK / 8 + NW - 1) / NW;  // ... of B
     constexpr int PPW = PPWB;
@@ -203,9 +201,9 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // 32 x 32 (16 registers each), or with the 16x16 shape 8 x 4 blocks of
     // 16 x 16 (4 registers each); the pod is the block's column = the lane
     // (mod PB), the node its row = register (+ lane group)
-    constexpr bool M16 = COST_MFMA16 != 0;
+    constexpr bool M16 = mfma16<DT>();
     constexpr int AM = M16 ? 8 : 4;
-    constexpr int AN = M16 ? 4 : NI;
+    constexpr int AN = M16 ? 2 * NI : NI;
     constexpr int AR = M16 ? 4 : 16;
     constexpr int PB = M16 ? 16 : 32;  // pods per block
     using accb_t = std::conditional_t<M16, typename M::acc4_t, acc_t>;
@@ -256,7 +254,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // the loop fills the 168 registers, and values held across it spilled)
     const int tid = threadIdx.x;
     int lane = tid & 63;
-    const int w = NWN == 6 ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+    const int w = WIDE ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
     const int wm = w / NWN, wn = w % NWN;
 
     const unsigned char *Ag = Lt + (size_t)mt * BM * Kb;
@@ -274,7 +272,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     auto bbuf = [&](int b) -> unsigned char * { return lds + b * STG + BM * BKB; };
     // one 1 KiB LDS-DMA piece (8 rows x 128 B) of operand A / B: piece j of
     // wave w fills rows (NW*j + w)*8 .. +8
-    // (saddr form, COST_NARROW_SADDR: rows r0 + l/8 of a piece all swizzle by
+    // (saddr form: rows r0 + l/8 of a piece all swizzle by
     // (4 * (r0 / 8) + l / 16) & 7 = (4 * (w & 1) + l / 16) & 7 -- NW is even --,
     // so one lane offset serves every piece of the wave, A and B alike)
     const unsigned loffn = (unsigned)(srow_in * Kb) +
@@ -282,15 +280,9 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     auto pieceA = [&](int buf, int k0, int j) {
         if (BM / 8 % NW && j * NW + w >= BM / 8) return;
         const int r0 = (j * NW + w) * 8;
-        if constexpr (COST_NARROW_SADDR && NW % 2 == 0) {
-            const int ru = __builtin_amdgcn_readfirstlane(r0);
-            glds16_s(Ag + (size_t)ru * Kb + k0, loffn,
-                     __builtin_amdgcn_readfirstlane(lds_off(abuf(buf) + r0 * BKB)));
-            return;
-        }
-        const int row = r0 + srow_in;
-        const int c = sq ^ ((row >> 1) & 7);
-        glds16(Ag + (size_t)row * Kb + k0 + c * 16, abuf(buf) + r0 * BKB);
+        const int ru = __builtin_amdgcn_readfirstlane(r0);
+        glds16_s(Ag + (size_t)ru * Kb + k0, loffn,
+                 __builtin_amdgcn_readfirstlane(lds_off(abuf(buf) + r0 * BKB)));
     };
     int bpod[PPW];  // RMAP: the WA rows of this lane's B pieces
     if constexpr (RMAP) {
@@ -301,7 +293,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     auto pieceB = [&](int buf, int k0, int j) {
         if (BNK / 8 % NW && j * NW + w >= BNK / 8) return;
         const int r0 = (j * NW + w) * 8;
-        if constexpr (!RMAP && COST_NARROW_SADDR && NW % 2 == 0) {
+        if constexpr (!RMAP) {
             const int ru = __builtin_amdgcn_readfirstlane(r0);
             glds16_s(Bg + (size_t)ru * Kb + k0, loffn,
                      __builtin_amdgcn_readfirstlane(lds_off(bbuf(buf) + r0 * BKB)));
@@ -325,14 +317,10 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         if (pj >= (BM + BNK) / 8) return;
         const unsigned char *base = pj < BM / 8 ? Ag + (size_t)pj * 8 * Kb
                                                 : Bg + (size_t)(pj - BM / 8) * 8 * Kb;
-#if COST_WIDE_SADDR
         glds16_s(base + k0, loff, __builtin_amdgcn_readfirstlane(lds_off(lds + buf * STG + pj * 8 * BKB)));
-#else
-        glds16(base + k0 + loff, lds + buf * STG + pj * 8 * BKB);
-#endif
     };
     auto stageA = [&](int buf, int k0) {
-        if constexpr (NWN == 6) {
+        if constexpr (WIDE) {
 #pragma unroll
             for (int j = 0; j < ((BM + BNK) / 8 + NW - 1) / NW; ++j) piece6(buf, k0, j);
         } else {
@@ -341,7 +329,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         }
     };
     auto stageB = [&](int buf, int k0) {
-        if constexpr (NWN != 6) {  // (the wide tile's stageA stages both)
+        if constexpr (!WIDE) {  // (the wide tile's stageA stages both)
 #pragma unroll
             for (int j = 0; j < PPW; ++j) pieceB(buf, k0, j);
         }
@@ -465,7 +453,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     // cost workgroup only while its two waves per SIMD leave registers free
     // (at 256 VGPRs the G = 8 rehearsal pass rose from 1.39 to 1.50 ms:
     // profiles/r03_bisect_g8.txt))
-    constexpr bool OVF_ROUND2 = NWN == 6 || !FUSE;
+    constexpr bool OVF_ROUND2 = WIDE || !FUSE;
     if constexpr (OVF_ROUND2 && DT == NAS_DT_I8) {
         if (ov.ptr) {
             const int cnt_lim = ov.row_count ? *ov.row_count : 0x7fffffff;
@@ -537,7 +525,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             }
         }
     };
-    if constexpr (NWN == 6) load_mask();
+    if constexpr (WIDE) load_mask();
 
     // fragments of k-substep kk+1 are read from LDS while the 8 MFMAs of kk
     // run (register double buffer)
@@ -576,30 +564,16 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         // ((2 kk + fh) ^ ((r >> 1) & 7)) * 16 = (row0 * BKB + ((fh ^ s) << 4)) ^
         // (kk << 5) + mi * 4096 with s = (fr >> 1) & 7 (the same for every mi,
         // ni and both operands): one lane offset per operand, an XOR per
-        // substep and immediate offsets (COST_XOR_FRAG)
+        // substep and immediate offsets
         auto read = [&](int kk, v4i (&ra)[4], v4i (&rb)[NI]) {
-            if constexpr (COST_XOR_FRAG) {
-                const unsigned ao = ((unsigned)((wm * 128 + fr) * BKB) + (unsigned)((fh ^ ((fr >> 1) & 7)) << 4)) ^ (unsigned)(kk << 5);
-                const unsigned bo = ((unsigned)((wn * WPODS + fr) * BKB) + (unsigned)((fh ^ ((fr >> 1) & 7)) << 4)) ^ (unsigned)(kk << 5);
+            const unsigned ao = ((unsigned)((wm * 128 + fr) * BKB) + (unsigned)((fh ^ ((fr >> 1) & 7)) << 4)) ^ (unsigned)(kk << 5);
+            const unsigned bo = ((unsigned)((wn * WPODS + fr) * BKB) + (unsigned)((fh ^ ((fr >> 1) & 7)) << 4)) ^ (unsigned)(kk << 5);
 #pragma unroll
-                for (int mi = 0; mi < 4; ++mi)
-                    ra[mi] = *reinterpret_cast<const v4i *>(As + ao + mi * 32 * BKB);
+            for (int mi = 0; mi < 4; ++mi)
+                ra[mi] = *reinterpret_cast<const v4i *>(As + ao + mi * 32 * BKB);
 #pragma unroll
-                for (int ni = 0; ni < NI; ++ni)
-                    rb[ni] = *reinterpret_cast<const v4i *>(Bs + bo + ni * 32 * BKB);
-                return;
-            }
-            const int c = kk * 2 + fh;
-#pragma unroll
-            for (int mi = 0; mi < 4; ++mi) {
-                const int r = wm * 128 + mi * 32 + fr;
-                ra[mi] = *reinterpret_cast<const v4i *>(As + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
-            }
-#pragma unroll
-            for (int ni = 0; ni < NI; ++ni) {
-                const int r = wn * WPODS + ni * 32 + fr;
-                rb[ni] = *reinterpret_cast<const v4i *>(Bs + r * BKB + ((c ^ ((r >> 1) & 7)) << 4));
-            }
+            for (int ni = 0; ni < NI; ++ni)
+                rb[ni] = *reinterpret_cast<const v4i *>(Bs + bo + ni * 32 * BKB);
         };
         read(0, a[0], bb[0]);
 #pragma unroll
@@ -619,7 +593,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     stageA(0, 0);
     stageB(0, 0);
     seed_ovf();
-    if constexpr (NWN != 6) load_mask();
+    if constexpr (!WIDE) load_mask();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int t = 0; t < nk; ++t) {
@@ -633,7 +607,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         __syncthreads();
     }
 
-    if constexpr (NWN == 6) {
+    if constexpr (WIDE) {
         // the lane index afresh (volatile: not CSE'd with the prologue's), so
         // the old one dies in the loop
         int l;
@@ -661,9 +635,18 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
     auto noff = [&](int mi, int reg) -> int {
         return M16 ? mi * 16 + 4 * fh + reg : mi * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * fh;
     };
-    u64 key[AN][8], bnd[AN];
+    // 16x16: each pod block's merged list goes to LDS as soon as it is made
+    // (lists of both node halves, [wm][wn][pod][9] u64, past the fused fit's
+    // words: the second staging image is dead), so no block's list stays in
+    // registers beside the accumulators (held there, they spilled)
+    constexpr int XL_OFF = FIT_LDS_OFF + NW * AN * 2 * 64 * 8;
+    static_assert(!M16 || XL_OFF + 2 * NWN * WPODS * 9 * 8 <= 2 * STG, "16x16 list image");
+    u64 *xl = reinterpret_cast<u64 *>(lds + XL_OFF);
+    u64 key[M16 ? 1 : AN][8], bnd[M16 ? 1 : AN];
 #pragma unroll
     for (int ni = 0; ni < AN; ++ni) {
+        u64 (&kl)[8] = key[M16 ? 0 : ni];
+        u64 &bl = bnd[M16 ? 0 : ni];
         u64 mwf[2];
         if constexpr (FUSE) {
 #pragma unroll
@@ -792,46 +775,49 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         u64 o4[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) o4[j] = shfl_xor64(k4[j], M16 ? 16 : 32);
-        merge44(k4, o4, key[ni]);
-        bnd[ni] = umin64(k4[3], o4[3]);
+        merge44(k4, o4, kl);
+        bl = umin64(k4[3], o4[3]);
         if constexpr (M16) {  // the other two row groups (lanes l ^ 32)
             u64 o8[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o8[j] = shfl_xor64(key[ni][j], 32);
-            const u64 ob = shfl_xor64(bnd[ni], 32);
-            merge88(key[ni], o8);
-            bnd[ni] = umin64(umin64(bnd[ni], ob), key[ni][7]);
+            for (int j = 0; j < 8; ++j) o8[j] = shfl_xor64(kl[j], 32);
+            const u64 ob = shfl_xor64(bl, 32);
+            merge88(kl, o8);
+            bl = umin64(umin64(bl, ob), kl[7]);
+            // the four row groups now hold the same list: group ni & 3 stores it
+            if (fh == (ni & 3)) {
+                u64 *d = xl + ((size_t)(wm * NWN + wn) * WPODS + ni * 16 + fr) * 9;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) d[j] = kl[j];
+                d[8] = bl;
+            }
         }
     }
 
     // merge the two node-half waves (wm = 0, 1) through LDS
     u64 *xk = reinterpret_cast<u64 *>(lds);  // [wn][64 pods][9], staging is dead
     if constexpr (M16) {
-        // every lane holds all four pod blocks' lists; lane l takes pod l of
-        // the wave (block fh, pod fr): selected without a runtime index
-        // (which would put the lists in scratch)
-        u64 mine[8], b;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            mine[j] = fh == 0 ? key[0][j] : fh == 1 ? key[1][j] : fh == 2 ? key[2][j] : key[3][j];
-        b = fh == 0 ? bnd[0] : fh == 1 ? bnd[1] : fh == 2 ? bnd[2] : bnd[3];
-        u64 *d = xk + (size_t)(wn * WPODS + lane) * 9;
-        if (wm == 1) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) d[j] = mine[j];
-            d[8] = b;
-        }
+        // lane l of a wm = 0 wave merges pod 64 rr + l's two node-half lists
         __syncthreads();
         if (wm == 0) {
-            u64 other[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) other[j] = d[j];
-            merge88(mine, other);
-            b = umin64(umin64(b, d[8]), mine[7]);
-            const int pod = p0 + nt * BNK + wn * WPODS + lane;
-            if (pod < p_end) {
-                store8(partial + ((size_t)mt * Pp + pod) * KC, mine);
-                pbound[(size_t)mt * Pp + pod] = b;
+            for (int rr = 0; rr < (WPODS + 63) / 64; ++rr) {
+                if (rr * 64 + lane >= WPODS) continue;
+                const u64 *d0 = xl + ((size_t)wn * WPODS + rr * 64 + lane) * 9;
+                const u64 *d1 = d0 + (size_t)NWN * WPODS * 9;
+                u64 mine[8], other[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    mine[j] = d0[j];
+                    other[j] = d1[j];
+                }
+                merge88(mine, other);
+                const u64 bb = umin64(umin64(d0[8], d1[8]), mine[7]);
+                const int pod = p0 + nt * BNK + wn * WPODS + rr * 64 + lane;
+                if (pod < p_end) {
+                    store8(partial + ((size_t)mt * Pp + pod) * KC, mine);
+                    pbound[(size_t)mt * Pp + pod] = bb;
+                }
             }
         }
         return;
@@ -863,9 +849,9 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             pbound[(size_t)mt * Pp + pod] = b;
         };
 #pragma unroll
-        for (int rr = 0; rr < NI / 2; ++rr) {
+        for (int rr = 0; rr < (NI + 1) / 2; ++rr) {
             if (fh == 0) finish(key[2 * rr], bnd[2 * rr], 2 * rr, rr);
-            else finish(key[2 * rr + 1], bnd[2 * rr + 1], 2 * rr + 1, rr);
+            else if (2 * rr + 1 < NI) finish(key[2 * rr + 1], bnd[2 * rr + 1], 2 * rr + 1, rr);
         }
     }
     }
@@ -948,6 +934,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
                          uint64_t *pbound, int node_base, const Dyn *dyn, int batch,
                          const Ovf &ov, const int32_t *rowmap, const FitSrc &fs = FitSrc{}) {
     constexpr int BNK = NWN * 64;
+    constexpr bool WIDE = BNK > BN;
     const void *fn = reinterpret_cast<const void *>(&k_cost_topk<DT, RMAP, NWN, FUSE>);
     constexpr int lds = 2 * (BM + BNK) * BKB;
     static std::atomic<unsigned long long> attr_set{0};
@@ -956,7 +943,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const int n_mt = Mp / BM, n_nt = (np + BNK - 1) / BNK;
     // the wide tile's last pod tile reads up to WA_PAD_ROWS rows past the
     // launch; past the last cluster's Pp rows only the padding is allocated
-    if (NWN == 6 && (int64_t)p0 + (int64_t)n_nt * BNK > (int64_t)Pp + WA_PAD_ROWS)
+    if (WIDE && (int64_t)p0 + (int64_t)n_nt * BNK > (int64_t)Pp + WA_PAD_ROWS)
         return hipErrorInvalidValue;
     // the fused fit (the wide tile always): capacity and requests
     if (FUSE && (!fs.cap || !fs.req || fs.nloc > Mp || fs.n0 + fs.nloc > fs.N || dyn))
@@ -970,7 +957,7 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     const int dh = dyn ? dyn->hi : 0;
     const int *dhp = dyn ? dyn->hi_ptr : nullptr;
     // the wide tile's launch end rides in dyn_hi (unused without a window)
-    const int dhi = NWN == 6 ? p0 + np : dh;
+    const int dhi = WIDE ? p0 + np : dh;
     k_cost_topk<DT, RMAP, NWN, FUSE><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
         lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dhi, dhp, ov, rowmap, fs);
     return hipGetLastError();
