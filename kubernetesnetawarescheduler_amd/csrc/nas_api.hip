@@ -360,8 +360,9 @@ int tile_pods(const nas_ctx *ctx) {
 // between two cost launches of a scoring stream; windows keep the k_fit mask.
 hipError_t launch_cost(nas_ctx *ctx, hipStream_t st, int Pp, int p0, int np, const uint64_t *mask,
                        const nas::Dyn *dyn, int batch, const nas::Ovf *ov,
-                       const int32_t *rowmap = nullptr, const nas::FitSrc *fit = nullptr) {
-    const bool wide = wide_ok(ctx);
+                       const int32_t *rowmap = nullptr, const nas::FitSrc *fit = nullptr,
+                       bool narrow = false) {
+    const bool wide = !narrow && wide_ok(ctx);
     if (ctx->dtype == NAS_DT_F32)
         return nas::launch_cost_topk(st, NAS_DT_BF16, ctx->Lt6.p, ctx->WA6.p, ctx->Mp, 6 * ctx->Kp,
                                      Pp, p0, np, mask, ctx->partial.as<uint64_t>(),
@@ -863,7 +864,13 @@ int score_batch(nas_ctx *ctx, Timer &tm) {
     hipEvent_t e1 = e0;
     const nas::Ovf ov = make_ovf(ctx);
     const nas::FitSrc fit{ctx->cap.as<int32_t>(), ctx->req.as<int32_t>(), N, 0, N};
-    HIPCK(launch_cost(ctx, st, Pp, 0, Pp, mask, nullptr, B, &ov, nullptr, &fit));
+    // whole wide tiles (384 pods) over the pods a multiple of 768 (a launch
+    // covers 256-pod units) reaches, 256 x 256 tiles over the rest: C5's 5,000
+    // pods (Pp 5,120) are 12 wide + 2 narrow tiles per cluster instead of 14
+    // wide ones, the last of them 8 pods of 384
+    const int W = tile_pods(ctx) != nas::COST_BN ? Pp / 768 * 768 : 0;
+    if (W > 0) HIPCK(launch_cost(ctx, st, Pp, 0, W, mask, nullptr, B, &ov, nullptr, &fit));
+    if (W < Pp) HIPCK(launch_cost(ctx, st, Pp, W, Pp - W, mask, nullptr, B, &ov, nullptr, &fit, true));
     hipEvent_t e2 = tm.mark(st);
     const int n_lists = ctx->Mp / nas::COST_BM;
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
@@ -2233,7 +2240,15 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
                                  last && status_in_commit ? hs : nullptr));
         tm.span(T_COMMIT, c0, tm.fine(cs));
         // the commit wrote this chunk's results into the pinned stage as it
-        // ended, and the host unpacks them while later chunks still run
+        // ended, and the host unpacks them while later chunks still run.
+        // Stage ordering rule: every stage row the host reads
+        // has ONE writer in the pass -- this commit kernel (to_stage), or
+        // fetch()'s copies on `st` issued after the host has waited for every
+        // landed event -- and the host reads it only after waiting on an
+        // event recorded on the writer's stream behind the writer.  No D2H
+        // copy into the stage runs on a scoring stream (round 4's TAIL_SDMA
+        // variant moved the last chunk's rows to such a copy and returned
+        // stale rows: profiles/r05e_stage_order_probe.txt)
         landed.push_back({lo, hi, tm.mark(cs)});
     }
     // st must follow everything: the last chunk's stream followed the commit

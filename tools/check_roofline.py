@@ -42,9 +42,16 @@ def expected(name, cfg, nodes, pods):
         return DT["bf16"], grid_x(nodes, pods), 1
     if name == "C2_f32":  # the fp32 split runs the bf16 kernel
         return DT["bf16"], grid_x(1000, 10000), 1
-    if name == "C5":
-        return DT["i8"], grid_x(5000, 5000, 64), 64
+    if name == "C5":  # first launch of the wide + narrow pair (score_batch)
+        return DT["i8"], cdiv(5000, BM) * (cdiv(5000, BN) * BN // 768 * 2) * 768, 64
     raise KeyError(name)
+
+
+def c5_narrow_grid():
+    """the narrow launch behind C5's wide one: 256 x 256 tiles over the pods
+    past the last multiple of 768 (5,120 padded pods: 512 of them)"""
+    pp = cdiv(5000, BN) * BN
+    return cdiv(5000, BM) * ((pp - pp // 768 * 768) // BN) * 512
 
 
 def main():
@@ -77,6 +84,14 @@ def main():
             res[name] = {"error": f"{len(ds)} matching dispatches, bench timed {n}"}
             continue
         ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in ds[-n:]]
+        if name == "C5":  # the bench's span covers the wide launch and the narrow one behind it
+            nx = [r for r in rows if tag in r["Kernel_Name"] and int(r["Grid_Size_X"]) == c5_narrow_grid()
+                  and int(r["Grid_Size_Y"]) == gy]
+            if len(nx) < n:
+                res[name] = {"error": f"{len(nx)} narrow dispatches, bench timed {n}"}
+                continue
+            ms = [(int(b["End_Timestamp"]) - int(a["Start_Timestamp"])) * 1e-6
+                  for a, b in zip(ds[-n:], nx[-n:])]
         prof = sum(ms) / n
         ops = rf.get("ops_per_launch")
         peak = rf["peak"]
