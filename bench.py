@@ -348,7 +348,11 @@ def bench_fit_kernel(args, d, eng, reps=10):
     filter as its own HBM-bound kernel.  Algorithmic bytes: the mask written
     once (P x ceil(N/64) x 8 B) plus capacities and requests read once."""
     N, P = args.nodes, args.pods
-    nloc = (d.rank + 1) * N // d.world - d.rank * N // d.world
+    # the filter covers this context's node shard (a rehearsal's rank 0 holds
+    # the first N / G nodes)
+    G = args.rehearse_world or d.world
+    r = 0 if args.rehearse_world else d.rank
+    nloc = (r + 1) * N // G - r * N // G
     eng.reset_capacity()
     eng.filter(want_mask=False)  # warm-up
     ms = []
