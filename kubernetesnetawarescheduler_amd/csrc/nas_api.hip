@@ -1047,6 +1047,10 @@ void inject_stall(nas_ctx *ctx, hipStream_t st) {
 // about 32, so the commit left after the scoring ends (the serial tail, which
 // matters most on a node shard's short scoring) is short.
 constexpr int CHUNK_WORKGROUPS = 512;  // cost workgroups per big chunk (measured best)
+// a node shard's chunks after the first, on shards of up to
+// SHARD_CHUNKS_MAX_MT node tiles (C3 from G = 4 on)
+constexpr int SHARD_CHUNKS = 6;
+constexpr int SHARD_CHUNKS_MAX_MT = 10;
 // 256-pod units per chunk on the wide tile: 32 tiles of 384 (1,280 workgroups
 // at 40 node tiles, as the 256-pod form's 32-unit chunks); 24 / 33 units
 // measured 0.5-2% slower (profiles/r02_s4_ab_chunk.txt)
@@ -1090,11 +1094,19 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
         // the first part would be a sliver of under 16)
         if (c > 0 && left > 32 && left <= big && left - 32 >= 16) tiles = left - 32;
     } else if (mode == 2 && c > 0) {
-        // the rest in equal chunks of at most `big` tiles (a short last chunk
-        // of 16 / 32 tiles, to shorten the commit left after the scoring,
+        // the rest in equal chunks: SHARD_CHUNKS of them (counting from
+        // chunk 1; fewer when a chunk would drop below 32 units) on shards of
+        // up to SHARD_CHUNKS_MAX_MT node tiles, else of at most `big` tiles
+        // (~512 workgroups).  Six measured best on the C3 rehearsal: G = 8
+        // 1.213 vs 1.227 ms, G = 4 2.105 vs 2.174 ms, but G = 3 (14 node
+        // tiles, 560-workgroup chunks) 2.850 vs 2.812 ms; three to seven
+        // swept (profiles/r05ab_ab_shard_chunks.txt).  (A short last chunk of
+        // 16 / 32 tiles, to shorten the commit left after the scoring,
         // measured 7-13% slower at G = 8 and 2-3% at G = 4: one more chunk
         // costs more cross-stream hops than its shorter commit saves)
-        const int n = (left + big - 1) / big;
+        const int n = n_mt <= SHARD_CHUNKS_MAX_MT
+                          ? std::max(1, std::min(SHARD_CHUNKS - c + 1, left / 32))
+                          : (left + big - 1) / big;
         tiles = (left + n - 1) / n;
     }  // (decreasing chunk sizes n, n-1, ..., 1 measured 7-10% slower at G = 4 / 8)
     // whole cost tiles per chunk: the wide tile (384 pods) needs multiples of
