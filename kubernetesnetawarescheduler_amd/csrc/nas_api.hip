@@ -1197,7 +1197,7 @@ int alloc_extended(nas_ctx *ctx) {
     OK(nas::ensure(ctx, ctx->status, std::max<size_t>(256, B * nas::STATUS_INTS * 4)));
     OK(nas::ensure(ctx, ctx->cap_snap, (size_t)3 * ctx->N * 4));
     if (exchanging(ctx)) {
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < 3; ++i) {
             OK(nas::ensure(ctx, ctx->gather[i], (size_t)ctx->world * ctx->Pp * (KC + 1) * 8));
             OK(nas::ensure(ctx, ctx->gbound[i], (size_t)ctx->world * ctx->Pp * 8));
         }
@@ -1381,7 +1381,8 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->stream_commit, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+        hipStreamCreateWithPriority(&ctx->stream_commit, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stream_x, hipStreamNonBlocking, prio_hi) != hipSuccess) {
         delete ctx;
         return NAS_ERR_HIP;
     }
@@ -1393,13 +1394,15 @@ void nas_destroy(nas_ctx *ctx) {
     NAS_RANGE("nas_destroy");
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream_commit}) (void)hipStreamSynchronize(st);
+    for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream_commit, ctx->stream_x})
+        if (st) (void)hipStreamSynchronize(st);
     DevBuf *bufs[] = {&ctx->snap[0], &ctx->snap[1], &ctx->snap[2], &ctx->snap[3], &ctx->snap[4],
                       &ctx->snap[5], &ctx->order1, &ctx->pos1, &ctx->order2, &ctx->pos2,
                       &ctx->pod_snap, &ctx->best, &ctx->winners, &ctx->snap_best, &ctx->snap_win,
                       &ctx->Lt, &ctx->WA, &ctx->cap0, &ctx->cap, &ctx->cap_snap, &ctx->req, &ctx->mask,
                       &ctx->partial, &ctx->pbound, &ctx->cand_key, &ctx->cand_bound,
                       &ctx->gather[0], &ctx->gbound[0], &ctx->gather[1], &ctx->gbound[1],
+                      &ctx->gather[2], &ctx->gbound[2], &ctx->xsend[2],
                       &ctx->resc_key, &ctx->resc_bound, &ctx->gather_r, &ctx->gbound_r,
                       &ctx->out_node, &ctx->out_cost_f, &ctx->out_cost_i,
                       &ctx->g_words, &ctx->g_idx, &ctx->g_key,
@@ -1417,6 +1420,7 @@ void nas_destroy(nas_ctx *ctx) {
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->stream2);
     (void)hipStreamDestroy(ctx->stream_commit);
+    if (ctx->stream_x) (void)hipStreamDestroy(ctx->stream_x);
     delete ctx;
 }
 
@@ -2221,6 +2225,19 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // pass: the host must wait on st then)
     // (the pass's last commit writes the status words to the pinned host area)
     const bool status_in_commit = spec == 0 && ctx->opt_inject_stall_ms == 0;
+    // A node-shard pass's chunks merge and exchange on their own stream (sx,
+    // the commit stream's communicator and CUs) and the commit stream only
+    // commits, each commit waiting for its chunk's merged lists: with every
+    // chunk's merge -> all-gather -> merge -> commit chain on the commit
+    // stream the chains of the last two chunks ran back to back after the
+    // scoring (~108 us each at G = 8 with six shard chunks); now one chunk's
+    // exchange overlaps the previous chunk's commit.  The tail chunk merges
+    // and exchanges on its scoring stream right behind its cost launch (its
+    // stream's own communicator and gather buffers, so the collectives of
+    // each communicator stay on one stream in one order) and commits there
+    // after the commit stream's last commit.
+    const bool xs_mode = exchanging(ctx) && !one_stream;
+    const hipStream_t sx = ctx->stream_x;
     for (size_t c = 0; c < chunks.size(); ++c) {
         const int lo = chunks[c].first, hi = chunks[c].second;
         // the last chunk is merged and committed on its own scoring stream
@@ -2231,16 +2248,30 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         const bool tail = !one_stream && c + 1 == chunks.size();
         const bool last = c + 1 == chunks.size();
         hipStream_t cs = sc;
-        if (tail) {
-            cs = ss2[c & 1];
-            HIPCK(hipStreamWaitEvent(cs, tm.mark(sc), 0));
-        } else if (!one_stream) {
-            HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
+        if (xs_mode) {
+            if (tail) {
+                cs = ss2[c & 1];
+                OK(merge_range(ctx, tm, lo, hi, cs, (c & 1) ? CH_SCORE2 : CH_SCORE, (int)(c & 1),
+                               main_view(ctx)));
+                HIPCK(hipStreamWaitEvent(cs, tm.mark(sc), 0));
+            } else {
+                HIPCK(hipStreamWaitEvent(sx, scored[c], 0));
+                OK(merge_range(ctx, tm, lo, hi, sx, CH_COMMIT, 2, main_view(ctx)));
+                HIPCK(hipStreamWaitEvent(sc, tm.mark(sx), 0));
+            }
+        } else {
+            if (tail) {
+                cs = ss2[c & 1];
+                HIPCK(hipStreamWaitEvent(cs, tm.mark(sc), 0));
+            } else if (!one_stream) {
+                HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
+            }
+            // (merging the tail chunk locally before this wait, gated before
+            // its exchange / commit, measured within noise at G = 1 and 8:
+            // profiles/r04_ab_tail.txt)
+            OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx),
+                           init_in_merge ? halt : nullptr));
         }
-        // (merging the tail chunk locally before this wait, gated before its
-        // exchange / commit, measured within noise at G = 1 and 8:
-        // profiles/r04_ab_tail.txt)
-        OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx), init_in_merge ? halt : nullptr));
         hipEvent_t c0 = tm.fine(cs);
         // the pass's last commit also writes the status words into the pinned
         // host area when nothing follows it (no speculative slots): the host
@@ -2264,8 +2295,9 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         landed.push_back({lo, hi, tm.mark(cs)});
     }
     // st must follow everything: the last chunk's stream followed the commit
-    // stream, which followed every earlier chunk's scoring; so st waits only
-    // when the last chunk ran on another stream
+    // stream, which followed every earlier chunk's scoring (and, with xs_mode,
+    // every earlier chunk's exchange); so st waits only when the last chunk
+    // ran on another stream
     if (!one_stream && ss2[(chunks.size() - 1) & 1] != st)
         HIPCK(hipStreamWaitEvent(st, tm.mark(ss2[(chunks.size() - 1) & 1]), 0));
     if (has_coll(ctx)) inject_stall(ctx, st);  // behind every collective of the pass
@@ -2554,21 +2586,24 @@ int set_stream_masks(nas_ctx *ctx, int reserve) {
     HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
     if (reserve > 0 && (ncu % 8 || ncu / 8 <= 2 * reserve)) reserve = 0;  // not an 8-XCD part
     if (reserve == ctx->cu_reserve) return NAS_OK;
-    for (hipStream_t s : {ctx->stream, ctx->stream2, ctx->stream_commit}) HIPCK(hipStreamSynchronize(s));
-    hipStream_t ns[3] = {nullptr, nullptr, nullptr};
+    for (hipStream_t s : {ctx->stream, ctx->stream2, ctx->stream_commit, ctx->stream_x})
+        HIPCK(hipStreamSynchronize(s));
+    // (the exchange stream shares the commit stream's CUs)
+    hipStream_t ns[4] = {nullptr, nullptr, nullptr, nullptr};
     hipError_t e = hipSuccess;
     if (reserve > 0) {
         const int words = (ncu + 31) / 32;
         std::vector<uint32_t> ms(words, 0), mc(words, 0);
         for (int b = 0; b < ncu; ++b) (b < 8 * reserve ? mc : ms)[b / 32] |= 1u << (b % 32);
-        for (int i = 0; i < 3 && e == hipSuccess; ++i)
-            e = hipExtStreamCreateWithCUMask(&ns[i], (uint32_t)words, i == 2 ? mc.data() : ms.data());
+        for (int i = 0; i < 4 && e == hipSuccess; ++i)
+            e = hipExtStreamCreateWithCUMask(&ns[i], (uint32_t)words, i >= 2 ? mc.data() : ms.data());
     } else {
         int lo = 0, hi = 0;
         e = hipDeviceGetStreamPriorityRange(&lo, &hi);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&ns[0], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&ns[1], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithPriority(&ns[2], hipStreamNonBlocking, hi);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&ns[3], hipStreamNonBlocking, hi);
     }
     if (e != hipSuccess) {
         for (hipStream_t s : ns)
@@ -2578,9 +2613,11 @@ int set_stream_masks(nas_ctx *ctx, int reserve) {
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->stream2);
     (void)hipStreamDestroy(ctx->stream_commit);
+    (void)hipStreamDestroy(ctx->stream_x);
     ctx->stream = ns[0];
     ctx->stream2 = ns[1];
     ctx->stream_commit = ns[2];
+    ctx->stream_x = ns[3];
     ctx->cu_reserve = reserve;
     return NAS_OK;
 }

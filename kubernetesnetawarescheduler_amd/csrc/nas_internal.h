@@ -95,6 +95,9 @@ struct nas_ctx {
     hipStream_t stream = nullptr;      // main stream (uploads, scoring, results)
     hipStream_t stream2 = nullptr;     // second scoring stream (chunk tails overlap)
     hipStream_t stream_commit = nullptr;  // commit walks, pipelined behind scoring
+    // a node-shard pass's chunk merges and all-gathers, ahead of their commits
+    // (so one chunk's exchange runs beside the previous chunk's commit)
+    hipStream_t stream_x = nullptr;
     int32_t cu_reserve = 0;               // CUs per XCD kept for stream_commit (set_stream_masks)
     std::string err;
     hipEvent_t ev[12] = {};
@@ -121,7 +124,7 @@ struct nas_ctx {
     nas::DevBuf pod_snap, best, winners;
     nas::DevBuf snap_best, snap_win;  // per-snapshot results
     nas::DevBuf vote_part, vote_gather;
-    nas::DevBuf xsend[2];  // per gather slot: a chunk's lists to all-gather, [np][8] keys | [np] bounds  // node-shard partial records [S], [world][S]
+    nas::DevBuf xsend[3];  // per gather slot: a chunk's lists to all-gather, [np][8] keys | [np] bounds  // node-shard partial records [S], [world][S]
 
     // ---- extended mode
     int32_t N = 0;           // nodes
@@ -145,8 +148,8 @@ struct nas_ctx {
     nas::DevBuf pbound;      // [Mp/BM][Pp] uint64 exactness bound per node tile
     nas::DevBuf cand_key;    // [Pp][KC] uint64 (global node ids), after merge
     nas::DevBuf cand_bound;  // [Pp] uint64
-    nas::DevBuf gather[2];   // per scoring stream: [world][chunk][KC] uint64 (multi-GPU exchange)
-    nas::DevBuf gbound[2];   // per scoring stream: [world][chunk] uint64
+    nas::DevBuf gather[3];   // per scoring stream: [world][chunk][KC] uint64 (multi-GPU exchange)
+    nas::DevBuf gbound[3];   // per scoring stream: [world][chunk] uint64
     nas::DevBuf resc_key, resc_bound;      // rescore slot staging [win][KC] / [win] (multi-GPU)
     nas::DevBuf gather_r, gbound_r;        // rescore slot exchange [world][win][KC] / [world][win]
     nas::DevBuf out_node, out_cost_f, out_cost_i;  // [Pp]
