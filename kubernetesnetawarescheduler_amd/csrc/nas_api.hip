@@ -1381,8 +1381,7 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
         hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->stream_commit, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->stream_x, hipStreamNonBlocking, prio_hi) != hipSuccess) {
+        hipStreamCreateWithPriority(&ctx->stream_commit, hipStreamNonBlocking, prio_hi) != hipSuccess) {
         delete ctx;
         return NAS_ERR_HIP;
     }
@@ -2124,6 +2123,37 @@ int nas_score(nas_ctx *ctx) {
     return NAS_OK;
 }
 
+namespace {
+// The exchange stream of node-shard passes (nas_place), made on first use --
+// a world-1 context never has it: one more stream than the hardware queues a
+// process gets (4 on the pool's boxes) made a C3 world-1 pass 0.7% slower
+// (profiles/r05ae_ab_exchange_stream.txt) -- with the commit stream's CU mask
+// when the context reserves CUs for it, else at the commit stream's priority
+int exchange_stream(nas_ctx *ctx, hipStream_t *out) {
+    if (!ctx->stream_x) {
+        hipError_t e = hipSuccess;
+        if (ctx->cu_reserve > 0) {
+            int ncu = 0;
+            HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+            const int words = (ncu + 31) / 32;
+            std::vector<uint32_t> mc(words, 0);
+            for (int b = 0; b < 8 * ctx->cu_reserve && b < ncu; ++b) mc[b / 32] |= 1u << (b % 32);
+            e = hipExtStreamCreateWithCUMask(&ctx->stream_x, (uint32_t)words, mc.data());
+        } else {
+            int lo = 0, hi = 0;
+            e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+            if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx->stream_x, hipStreamNonBlocking, hi);
+        }
+        if (e != hipSuccess) {
+            ctx->stream_x = nullptr;
+            return nas::hip_fail(ctx, e, "exchange stream");
+        }
+    }
+    *out = ctx->stream_x;
+    return NAS_OK;
+}
+}  // namespace
+
 int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_score_out) {
     NAS_RANGE("nas_place");
     OK(bind(ctx));
@@ -2237,7 +2267,8 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // each communicator stay on one stream in one order) and commits there
     // after the commit stream's last commit.
     const bool xs_mode = exchanging(ctx) && !one_stream;
-    const hipStream_t sx = ctx->stream_x;
+    hipStream_t sx = nullptr;
+    if (xs_mode) OK(exchange_stream(ctx, &sx));
     for (size_t c = 0; c < chunks.size(); ++c) {
         const int lo = chunks[c].first, hi = chunks[c].second;
         // the last chunk is merged and committed on its own scoring stream
@@ -2587,23 +2618,21 @@ int set_stream_masks(nas_ctx *ctx, int reserve) {
     if (reserve > 0 && (ncu % 8 || ncu / 8 <= 2 * reserve)) reserve = 0;  // not an 8-XCD part
     if (reserve == ctx->cu_reserve) return NAS_OK;
     for (hipStream_t s : {ctx->stream, ctx->stream2, ctx->stream_commit, ctx->stream_x})
-        HIPCK(hipStreamSynchronize(s));
-    // (the exchange stream shares the commit stream's CUs)
-    hipStream_t ns[4] = {nullptr, nullptr, nullptr, nullptr};
+        if (s) HIPCK(hipStreamSynchronize(s));
+    hipStream_t ns[3] = {nullptr, nullptr, nullptr};
     hipError_t e = hipSuccess;
     if (reserve > 0) {
         const int words = (ncu + 31) / 32;
         std::vector<uint32_t> ms(words, 0), mc(words, 0);
         for (int b = 0; b < ncu; ++b) (b < 8 * reserve ? mc : ms)[b / 32] |= 1u << (b % 32);
-        for (int i = 0; i < 4 && e == hipSuccess; ++i)
-            e = hipExtStreamCreateWithCUMask(&ns[i], (uint32_t)words, i >= 2 ? mc.data() : ms.data());
+        for (int i = 0; i < 3 && e == hipSuccess; ++i)
+            e = hipExtStreamCreateWithCUMask(&ns[i], (uint32_t)words, i == 2 ? mc.data() : ms.data());
     } else {
         int lo = 0, hi = 0;
         e = hipDeviceGetStreamPriorityRange(&lo, &hi);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&ns[0], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&ns[1], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipStreamCreateWithPriority(&ns[2], hipStreamNonBlocking, hi);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&ns[3], hipStreamNonBlocking, hi);
     }
     if (e != hipSuccess) {
         for (hipStream_t s : ns)
@@ -2613,15 +2642,18 @@ int set_stream_masks(nas_ctx *ctx, int reserve) {
     (void)hipStreamDestroy(ctx->stream);
     (void)hipStreamDestroy(ctx->stream2);
     (void)hipStreamDestroy(ctx->stream_commit);
-    (void)hipStreamDestroy(ctx->stream_x);
+    // the exchange stream is made on first use, on the commit stream's CUs
+    if (ctx->stream_x) (void)hipStreamDestroy(ctx->stream_x);
+    ctx->stream_x = nullptr;
     ctx->stream = ns[0];
     ctx->stream2 = ns[1];
     ctx->stream_commit = ns[2];
-    ctx->stream_x = ns[3];
     ctx->cu_reserve = reserve;
     return NAS_OK;
 }
 }  // namespace
+
+
 
 int nas_comm_unique_id(uint8_t id_out[128]) {
     NAS_RANGE("nas_comm_unique_id");
