@@ -430,7 +430,45 @@ __global__ void k_split6(const float *__restrict__ src, unsigned short *__restri
     }
 }
 
+// The pass's commits run in chunk order on two streams -- the commit stream,
+// then the tail chunk's own stream -- ordered by a device word instead of a
+// stream-wait packet (~10-20 us on the pass's critical path even when the
+// awaited event had long completed): after each commit the commit stream
+// stores the commit's sequence number (a kernel boundary behind the commit,
+// so its capacity and status writes are released first), and the tail
+// stream's commit is preceded by a wait until the word reaches the last one.
+// The wait is bounded: after FLAG_WAIT_TICKS (2 s of the 100 MHz real-time
+// clock) it stores an impossible halt word, which the pass reports as an
+// error instead of hanging.
+constexpr unsigned long long FLAG_WAIT_TICKS = 200000000ull;
+constexpr int FLAG_TIMEOUT_HALT = 0x7ffffff0;
+
+__global__ void k_flag_set(unsigned long long *flag, unsigned long long v) {
+    __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void k_flag_wait(const unsigned long long *flag, unsigned long long v, int *halt) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < v) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > FLAG_WAIT_TICKS) {
+            halt[0] = FLAG_TIMEOUT_HALT;
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_flag_set(hipStream_t st, uint64_t *flag, uint64_t v) {
+    k_flag_set<<<1, 1, 0, st>>>(reinterpret_cast<unsigned long long *>(flag), v);
+    return hipGetLastError();
+}
+
+hipError_t launch_flag_wait(hipStream_t st, const uint64_t *flag, uint64_t v, int32_t *halt) {
+    k_flag_wait<<<1, 1, 0, st>>>(reinterpret_cast<const unsigned long long *>(flag), v, halt);
+    return hipGetLastError();
+}
 
 hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
                             int n) {

@@ -1196,6 +1196,11 @@ int alloc_extended(nas_ctx *ctx) {
     OK(nas::ensure(ctx, ctx->out_cost_i, B * ctx->Pp * 4));
     OK(nas::ensure(ctx, ctx->status, std::max<size_t>(256, B * nas::STATUS_INTS * 4)));
     OK(nas::ensure(ctx, ctx->cap_snap, (size_t)3 * ctx->N * 4));
+    if (!ctx->commit_flag.p) {
+        OK(nas::ensure(ctx, ctx->commit_flag, 8));
+        HIPCK(hipMemset(ctx->commit_flag.p, 0, 8));
+        ctx->commit_seq = 0;
+    }
     if (exchanging(ctx)) {
         for (int i = 0; i < 3; ++i) {
             OK(nas::ensure(ctx, ctx->gather[i], (size_t)ctx->world * ctx->Pp * (KC + 1) * 8));
@@ -2267,6 +2272,16 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // each communicator stay on one stream in one order) and commits there
     // after the commit stream's last commit.
     const bool xs_mode = exchanging(ctx) && !one_stream;
+    // the tail chunk's stream waits for the commit stream's last commit: by
+    // the device word behind each commit (launch_flag_set / flag_wait) once a
+    // commit has run on the commit stream, else by an event (a one-chunk pass
+    // with a communicator: only the pass init is on the commit stream)
+    auto *cflag = ctx->commit_flag.as<uint64_t>();
+    auto after_commits = [&](hipStream_t s) -> int {
+        if (chunks.size() > 1) HIPCK(nas::launch_flag_wait(s, cflag, ctx->commit_seq, halt));
+        else HIPCK(hipStreamWaitEvent(s, tm.mark(sc), 0));
+        return NAS_OK;
+    };
     hipStream_t sx = nullptr;
     if (xs_mode) OK(exchange_stream(ctx, &sx));
     for (size_t c = 0; c < chunks.size(); ++c) {
@@ -2284,7 +2299,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
                 cs = ss2[c & 1];
                 OK(merge_range(ctx, tm, lo, hi, cs, (c & 1) ? CH_SCORE2 : CH_SCORE, (int)(c & 1),
                                main_view(ctx)));
-                HIPCK(hipStreamWaitEvent(cs, tm.mark(sc), 0));
+                OK(after_commits(cs));
             } else {
                 HIPCK(hipStreamWaitEvent(sx, scored[c], 0));
                 OK(merge_range(ctx, tm, lo, hi, sx, CH_COMMIT, 2, main_view(ctx)));
@@ -2293,7 +2308,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         } else {
             if (tail) {
                 cs = ss2[c & 1];
-                HIPCK(hipStreamWaitEvent(cs, tm.mark(sc), 0));
+                OK(after_commits(cs));
             } else if (!one_stream) {
                 HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
             }
@@ -2312,6 +2327,8 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
                                  ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
                                  1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr,
                                  last && status_in_commit ? hs : nullptr));
+        // (releases the tail chunk's commit)
+        if (!one_stream && !last) HIPCK(nas::launch_flag_set(cs, cflag, ++ctx->commit_seq));
         tm.span(T_COMMIT, c0, tm.fine(cs));
         // the commit wrote this chunk's results into the pinned stage as it
         // ended, and the host unpacks them while later chunks still run.
@@ -2331,6 +2348,9 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // ran on another stream
     if (!one_stream && ss2[(chunks.size() - 1) & 1] != st)
         HIPCK(hipStreamWaitEvent(st, tm.mark(ss2[(chunks.size() - 1) & 1]), 0));
+    // (the tail followed the commit stream by the device word, not a stream
+    // wait: st follows the commit stream itself)
+    if (!one_stream && chunks.size() > 1) HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
     if (has_coll(ctx)) inject_stall(ctx, st);  // behind every collective of the pass
     for (int r = 0; r < spec; ++r) OK(gathered_slot(ctx, tm, st, CH_SCORE, nullptr, P));
     if (spec > 0) {

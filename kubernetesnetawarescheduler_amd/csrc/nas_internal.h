@@ -157,6 +157,8 @@ struct nas_ctx {
     nas::DevBuf g_key, g_bound;  // gathered rescore view's lists (rows read in place, row map g_idx)
     nas::DevBuf g_gk, g_gb;                // gathered rescore exchange [world][R][KC] / [world][R]
     nas::DevBuf status;      // small device scratch for commit control
+    nas::DevBuf commit_flag;  // the pass's last commit sequence number (launch_flag_set)
+    uint64_t commit_seq = 0;  // host copy: sequence numbers only grow, across passes
     nas::DevBuf host_status; // pinned
     nas::DevBuf ref_stage;   // pinned: nas_score_reference results [P] best | [P][6] winners
     nas::DevBuf scratch;
@@ -315,6 +317,12 @@ hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t
 
 // start of a nas_place pass: status[0] = -1 (halt), status[1 .. 2*STATUS_INTS)
 // = 0; cap_snap[0, n) = cap[0, n) when cap_snap is non-null
+// the commit order across the commit stream and the tail chunk's stream
+// (k_misc.hip): flag_set stores v into *flag behind the stream's work so far,
+// flag_wait holds the stream until *flag >= v (bounded; on timeout it writes
+// an impossible halt word, reported as an error by the pass)
+hipError_t launch_flag_set(hipStream_t st, uint64_t *flag, uint64_t v);
+hipError_t launch_flag_wait(hipStream_t st, const uint64_t *flag, uint64_t v, int32_t *halt);
 hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
                             int n);
 // rehearsal: rank slots 1..G-1 of an all-gathered buffer [G][n] of keys
