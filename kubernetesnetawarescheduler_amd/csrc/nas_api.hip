@@ -344,7 +344,7 @@ constexpr int WIDE_MIN_PODS = 32768;
 // CUs per XCD to the commit stream (set_stream_masks), so the merge /
 // exchange / commit chain runs beside the wide cost tile instead of waiting
 // for one of its workgroups to drain (profiles/r04_ab_reserve.txt)
-constexpr int RESERVE_SHARD_CUS = 2;  // per XCD; 3 from 8 ranks up (shard_reserve)
+constexpr int RESERVE_SHARD_CUS = 2;  // per XCD; 3 from 4 ranks, 4 from 8 (shard_reserve)
 bool wide_ok(const nas_ctx *ctx) {
     const bool shard = ctx->world > 1 || ctx->rehearse > 1;
     if (ctx->B > 1) return !shard;
@@ -2611,14 +2611,17 @@ int nas_commit(nas_ctx *ctx, int32_t p_begin, int32_t *node_out, float *cost_out
 
 // ---------------------------------------------------------------- multi-GPU
 namespace {
-// CUs per XCD kept for the commit stream on a node shard of `world` ranks:
-// same-box A/B (profiles/r04_ab_reserve.txt), rank-0 rehearsal ms per pass at
-// reserve 0 (narrow tile) / 2 / 3 / 4: G = 2 4.13-4.21 / 3.92-3.97 /
-// 3.96-4.00 / 3.99-4.03, G = 4 2.27-2.29 / 2.19-2.20 / 2.20-2.22 /
-// 2.16-2.20, G = 8 1.28-1.32 / 1.27-1.28 / 1.24-1.26 / 1.24-1.29
+// CUs per XCD kept for the commit and exchange streams on a node shard of
+// `world` ranks: same-box A/B (profiles/r04_ab_reserve.txt), rank-0
+// rehearsal ms per pass at reserve 0 (narrow tile) / 2 / 3 / 4: G = 2
+// 4.13-4.21 / 3.92-3.97 / 3.96-4.00 / 3.99-4.03, G = 4 2.27-2.29 / 2.19-2.20
+// / 2.20-2.22 / 2.16-2.20, G = 8 1.28-1.32 / 1.27-1.28 / 1.24-1.26 /
+// 1.24-1.29.  With six shard chunks and the exchange stream (round 5) the
+// chains want one CU more: G = 8 4 vs 3 1.186 vs 1.196 ms, G = 4 3 vs 2
+// 2.107 vs 2.117 ms (profiles/r05an_ab_reserve.txt)
 int shard_reserve(int world) {
     if (world <= 1) return 0;
-    return world >= 8 ? RESERVE_SHARD_CUS + 1 : RESERVE_SHARD_CUS;
+    return world >= 8 ? RESERVE_SHARD_CUS + 2 : world >= 4 ? RESERVE_SHARD_CUS + 1 : RESERVE_SHARD_CUS;
 }
 // Recreate the context's three streams: reserve > 0 keeps `reserve` CUs of
 // every XCD for the commit stream alone and the rest for the two scoring
