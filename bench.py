@@ -15,6 +15,11 @@ on one fresh 10k-node snapshot per pod, 48 GB) is timed too and reported under
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+`--gpus N > 1` without a launcher (no WORLD_SIZE in the environment) starts
+the N rank processes itself (launch_ranks: RANK / LOCAL_RANK / WORLD_SIZE and
+a file:// rendezvous per child, before this process touches the GPU) and
+relays rank 0's line.
 """
 import argparse
 import json
@@ -60,8 +65,13 @@ def parse():
                     help="diagnostic at --gpus 1: time rank 0 of a G-GPU node-sharded pass "
                          "(its node columns; the other ranks' lists are shifted copies of its "
                          "own; placements not meaningful, RCCL over a one-rank communicator)")
+    ap.add_argument("--synth-profile", type=int, default=0, choices=[0, 1],
+                    help="generator of the C3 inputs (NAS_OPT_SYNTH_PROFILE): 0 racks / zones "
+                         "with bound peers (default), 1 uniform over the full int8 range "
+                         "(SURVEY.md §8(d)'s operand distribution; configs.C3_fullrange)")
     ap.add_argument("--only", choices=["place", "vote", "score", "pmc", "C1", "C2", "C2_f32",
-                                       "C3_bf16", "C5", "C4", "C4_shardG2"], default=None,
+                                       "C3_bf16", "C3_fullrange", "C5", "C4", "C4_shardG2"],
+                    default=None,
                     help="profile helper: run only one path (pmc: the score and vote legs, "
                          "what the in-run PMC passes profile)")
     ap.add_argument("--no-pmc", action="store_true",
@@ -69,8 +79,31 @@ def parse():
     return ap.parse_args()
 
 
+def _cgroup_cpus():
+    """CPU quota of this process's cgroup in CPUs (cgroup v2 cpu.max, else v1
+    cfs quota / period), or None when unlimited / unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = float(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = float(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_info():
-    """Host CPU model and the cores this process may use (for the CPU baselines)."""
+    """Host CPU model and the cores this process may use (for the CPU
+    baselines).  `affinity` is what sched_getaffinity shows -- the whole
+    machine on the GPU pool's boxes --, `usable` the box's CPU share the
+    baselines run on: OMP_NUM_THREADS as the pool exports it (16 per GPU), else
+    the cgroup CPU quota, else the affinity count."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -81,16 +114,31 @@ def cpu_info():
     except OSError:
         pass
     try:
-        usable = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        usable = os.cpu_count()
-    # the box's CPU share: OMP_NUM_THREADS (16 on the GPU pool; `nproc` reports
-    # it too), while affinity and os.cpu_count() show the whole machine
-    return {"model": model, "nproc": os.cpu_count(), "usable": usable,
-            "omp_num_threads": int(os.environ.get("OMP_NUM_THREADS", "0")) or None}
+        affinity = os.cpu_count()
+    quota = _cgroup_cpus()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or None
+    if omp:
+        usable, why = min(omp, affinity), (
+            "OMP_NUM_THREADS (the box's CPU share as the GPU pool exports it: 16 CPUs per GPU "
+            "of a machine whose affinity mask shows all of its cores; worker pools are sized to "
+            "that share, and threads past it only contend with the other GPUs' jobs)")
+    elif quota:
+        usable, why = max(1, min(int(quota), affinity)), "cgroup CPU quota"
+    else:
+        usable, why = affinity, "sched_getaffinity (no quota, no OMP_NUM_THREADS)"
+    return {"model": model, "nproc": os.cpu_count(), "affinity": affinity,
+            "cgroup_quota_cpus": quota, "omp_num_threads": omp, "usable": usable,
+            "usable_source": why}
 
 
-def pmc_traffic(args):
+def host_threads():
+    """Threads for the pods-parallel CPU baselines: every usable core."""
+    return cpu_info()["usable"] or 1
+
+
+def pmc_traffic(args, profile=0):
     """HBM-side bytes per launch of the dominant kernels, measured in this run:
     two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: they do not fit one
     pass on gfx950) over a child `bench.py --only pmc` of the same workload,
@@ -107,7 +155,9 @@ def pmc_traffic(args):
         return {}, "rocprofv3 not found"
     child = [sys.executable, os.path.abspath(__file__), "--only", "pmc", "--steps", "1",
              "--warmup", "0", "--no-pmc", "--nodes", str(args.nodes), "--pods", str(args.pods),
-             "--dtype", args.dtype, "--peers", str(args.peers)]
+             "--dtype", args.dtype, "--peers", str(args.peers), "--synth-profile", str(profile)]
+    if profile != args.synth_profile:  # (a config line's inputs: the score leg only)
+        child.append("--no-reference-mode")
     out = {}
     tmp = tempfile.mkdtemp(prefix="nas_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
@@ -140,6 +190,91 @@ def pmc_traffic(args):
         return out, None
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def visible_gpus():
+    """GPUs this process could use, counted without initialising the GPU
+    (torch.cuda.device_count does not, on this image); 0 without torch / GPUs."""
+    try:
+        import torch
+        return int(torch.cuda.device_count())
+    except Exception:  # noqa: BLE001 -- no torch / no runtime: the CPU rank logic
+        return 0
+
+
+def launch_ranks(child_argv, n, ndev, timeout_s=None, extra_env=None):
+    """Start n rank processes of `child_argv` (one per GPU: LOCAL_RANK = r mod
+    ndev, so more ranks than GPUs share them -- RCCL then refuses and bench.py
+    falls back to its host exchange) with RANK / LOCAL_RANK / WORLD_SIZE and a
+    file:// gloo rendezvous (NAS_DIST_INIT: no TCP port to collide).  Wait for
+    all of them; as soon as one exits non-zero (or the deadline passes) kill
+    the others, so no rank is left waiting for a dead peer; always reap.
+    Rank 0's stdout goes to a file (bench.py prints its one JSON line there);
+    every rank's stderr is inherited.  Returns (rc, rank 0's stdout): rc is
+    the first failing rank's exit code (128 + signal for a signal), else 0."""
+    import shutil
+    import subprocess
+    import tempfile
+    tmp = tempfile.mkdtemp(prefix="nas_ranks_", dir="/tmp")
+    out0 = os.path.join(tmp, "rank0.out")
+    procs, failed = [], None
+    try:
+        with open(out0, "w") as f0:
+            for r in range(n):
+                env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r % ndev if ndev else r),
+                           WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                           NAS_DIST_INIT="file://" + os.path.join(tmp, "rdv"),
+                           MASTER_ADDR="127.0.0.1", **(extra_env or {}))
+                procs.append(subprocess.Popen(child_argv, env=env,
+                                              stdout=f0 if r == 0 else subprocess.DEVNULL))
+            deadline = None if timeout_s is None else time.monotonic() + timeout_s
+            rcs = [None] * n
+            while any(rc is None for rc in rcs):
+                for i, p in enumerate(procs):
+                    if rcs[i] is None:
+                        rcs[i] = p.poll()
+                        if rcs[i] not in (None, 0) and failed is None:
+                            failed = rcs[i]
+                if failed is not None:
+                    break
+                if deadline is not None and time.monotonic() > deadline:
+                    failed = 124
+                    print(f"launch_ranks: deadline of {timeout_s} s passed", file=sys.stderr)
+                    break
+                time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+        text = open(out0).read() if os.path.exists(out0) else ""
+        shutil.rmtree(tmp, ignore_errors=True)
+    if failed is not None and failed < 0:
+        failed = 128 - failed
+    return (failed or 0), text
+
+
+def self_launch(args):
+    """`bench.py --gpus N` (N > 1) with no launcher: N rank processes of this
+    same command line, one per GPU (launch_ranks), started before this process
+    makes any GPU call; rank 0's JSON line is relayed on stdout (with
+    config.launcher saying so) and the exit code is the first failing rank's."""
+    ndev = visible_gpus()
+    print(f"bench.py: no WORLD_SIZE in the environment; starting {args.gpus} rank processes "
+          f"({ndev} GPU(s) visible, file:// rendezvous)", file=sys.stderr, flush=True)
+    rc, text = launch_ranks([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], args.gpus,
+                            ndev)
+    lines = [ln for ln in text.splitlines() if ln.startswith("{")]
+    if lines:
+        out = json.loads(lines[-1])
+        out.setdefault("config", {})["launcher"] = (
+            f"bench.py self-launch: {args.gpus} rank processes on {ndev} visible GPU(s), "
+            f"gloo file:// rendezvous")
+        print(json.dumps(out), flush=True)
+    elif rc == 0:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr)
+        rc = 1
+    return rc
 
 
 class Dist:
@@ -240,7 +375,7 @@ def bench_place(args, d, eng):
             eng.set_option("COMM_TIMEOUT_MS", 60000)
             uid = d.bcast_bytes(eng.comm_unique_id() if d.rank == 0 else None)
             eng.comm_init(uid, d.rank, d.world)
-            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers, profile=args.synth_profile)
             if args.rehearse_world > 1:
                 # the stand-in lists repeat this rank's few best nodes G times,
                 # so herds would drain them at once; with 64x capacity no list
@@ -265,10 +400,10 @@ def bench_place(args, d, eng):
             eng = Engine(d.local)
             eng.set_shard(d.rank, d.world)
             exchange = f"host gloo all-gather (RCCL failed: {err or 'on another rank'})"
-            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers, profile=args.synth_profile)
             return bench_place_host(args, d, eng) + (eng, exchange)
     else:
-        eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+        eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers, profile=args.synth_profile)
     keys = ("cost_ms", "fit_ms", "merge_ms", "commit_ms", "total_ms", "cost_launches",
             "rescore_rounds", "unschedulable")
     acc = dict.fromkeys(keys, 0.0)
@@ -450,7 +585,7 @@ def bench_host(args):
     status = np.zeros(n, np.int32)
     ptrs = [o.ctypes.data_as(C.c_void_p) for o in outs] + [status.ctypes.data_as(C.c_void_p)]
     cores = cpu_info()
-    threads = cores["omp_num_threads"] or min(16, cores["usable"] or 1)
+    threads = cores["usable"] or 1
 
     def run(t, reps=5):
         ms = []
@@ -533,7 +668,7 @@ def cpu_baseline_place(args, eng, gpu_nodes, N=None, dtype=None, first=64):
     import oracle
     N = N or args.nodes
     dtype = dtype or args.dtype
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     os.environ["OMP_NUM_THREADS"] = str(threads)
     _, L, cap, req = eng.read_inputs(0, 0, want_L=True)
     Ps, spent, t_total, pods_done = first, 0.0, 0.0, 0
@@ -550,6 +685,7 @@ def cpu_baseline_place(args, eng, gpu_nodes, N=None, dtype=None, first=64):
         Ps *= 2
     match = bool((gpu_nodes[:pods_done] == placements).all())
     return {"value": pods_done * N / t_total, "unit": "pair-scores/s", "cores": threads,
+            "cores_note": "every usable core (cpu.usable, cpu.usable_source)",
             "kind": "port",
             "sample": f"oracle/oracle.c or_place (sequential greedy, cost rows on {threads} "
                       f"OpenMP threads) on the first {pods_done} pods x {N} nodes of the same "
@@ -600,7 +736,7 @@ def cpu_baseline_vote(args, eng, ref):
                                 f"{loop_ns * 1e-6:.1f} ms",
                       "gpu_matches_oracle_on_sample": bool((best_g == b_g).all())}
     # the same loop pods-parallel over the host's cores (BASELINE.md plan)
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     os.environ["OMP_NUM_THREADS"] = str(threads)
     S = min(2048, eng.snap_count)
     snaps = [eng.read_snapshot(s) for s in range(S)]
@@ -613,7 +749,9 @@ def cpu_baseline_vote(args, eng, ref):
         t_par += time.perf_counter() - t0
         reps += 1
     out["pods_parallel"] = {"value": reps * S * N / t_par, "unit": "pair-scores/s",
-                            "cores": threads, "sample": f"or_vote_batch over {S} snapshots x {N} "
+                            "cores": threads,
+                            "cores_note": "every usable core (cpu.usable, cpu.usable_source)",
+                            "sample": f"or_vote_batch over {S} snapshots x {N} "
                                                         f"nodes, OpenMP over pods, {reps} reps",
                             "gpu_matches_oracle_on_sample": bool((b == best[:S]).all() and
                                                                  (w == win[:S]).all())}
@@ -819,6 +957,58 @@ def config_c3_bf16(args, d, eng):
                          "launch_ms": cost_ms, "launches": 3, "ops_per_launch": ops}}
 
 
+_TRAFFIC_FULLRANGE = {}
+
+
+def config_c3_fullrange(args, d, eng, sample=2048):
+    """The headline C3 shape (10k nodes x 100k pods, int8) on SURVEY.md
+    §8(d)'s own operand distribution: latency and traffic
+    uniform over the full int8 range (NAS_OPT_SYNTH_PROFILE 1 -- U{1..127}
+    for U[1, 1000] us, U{0..127} for U[0, 1)), no rack / zone locality and no
+    bound-peer structure.  The cost kernel is power-limited, so its rate
+    depends on operand entropy: this line states whether >= 1e11 pair scores/s
+    holds on full-range operands.  A placement pass timed like the headline,
+    its own k_cost_topk roofline (with its PMC traffic when collected) and the
+    first `sample` pods checked against the sequential oracle."""
+    import oracle
+    N, P = args.nodes, args.pods
+    eng.synth_cluster(SEED, N, P, "i8", peers=args.peers, profile=1)
+    t, res = _timed_place(d, eng, args.steps, args.warmup)
+    ms = t * 1e3 / args.steps
+    eng.reset_capacity()
+    cms = []
+    for _ in range(max(4, args.steps // 2 + 1)):
+        eng.score()
+        cms.append(eng.timings()["cost_ms"])
+    cost_ms = float(np.mean(cms[1:]))
+    ops = 2.0 * P * N * N
+    WA, L, cap, req = eng.read_inputs(0, sample, want_L=True)
+    t0 = time.perf_counter()
+    want, wcost, _ = oracle.place(WA, L, req[:sample], cap, "i8")
+    t_cpu = time.perf_counter() - t0
+    ok = bool((res["node"][:sample] == want).all() and (res["score"][:sample] == wcost).all())
+    tr = _TRAFFIC_FULLRANGE.get("k_cost_topk", {}).get("bytes")
+    value = P * N / (ms * 1e-3)
+    return {"workload": f"C3 on the full int8 range: {N} nodes x {P} pods, latency U{{1..127}} "
+                        f"(symmetric, zero diagonal), traffic U{{0..127}} to every node, "
+                        f"clusterloader2-shaped requests", "dtype": "i8xi8->i32",
+            "value": value, "unit": "pair-scores/s", "ms_per_step": ms,
+            "placements_per_s": P / (ms * 1e-3), "meets_1e11": bool(value >= 1e11),
+            "unschedulable": res["t"]["unschedulable"], "rescore_rounds": res["t"]["rescore_rounds"],
+            "matches_oracle": ok, "oracle_check": f"first {sample} pods: placements and scores",
+            "operands": {"WA_min": int(WA.min()), "WA_max": int(WA.max()),
+                         "WA_mean": float(WA.mean()), "L_offdiag_min": int(L[~np.eye(N, dtype=bool)].min()),
+                         "L_max": int(L.max()), "L_symmetric": bool((L == L.T).all())},
+            "roofline": {"kernel": "k_cost_topk<int8> (wide tile)", "bound": "mfma",
+                         "achieved": ops / (cost_ms * 1e-3) / 1e12, "peak": PEAK_I8_TOPS,
+                         "unit": "TFLOP/s", "frac": ops / (cost_ms * 1e-3) / 1e12 / PEAK_I8_TOPS,
+                         "traffic": tr, "traffic_unit": "B/launch",
+                         "launch_ms": cost_ms, "launches": len(cms) - 1, "ops_per_launch": ops},
+            "cpu_baseline": {"value": sample * N / t_cpu, "unit": "pair-scores/s",
+                             "cores": int(os.environ.get("OMP_NUM_THREADS", "1")), "kind": "port",
+                             "sample": f"oracle or_place on the first {sample} pods"}}
+
+
 def config_c2_f32(args, d, eng):
     """C2 with measured float latencies (microseconds, unquantised) and float
     traffic (MB): the fp32 path (v_mfma_f32_32x32x2_f32, exact fp32 products).
@@ -952,7 +1142,8 @@ def run_configs(args, d, only=None):
     from kubernetesnetawarescheduler_amd import Engine
     out = {}
     for name, fn in (("C1", config_c1), ("C2", config_c2), ("C2_f32", config_c2_f32),
-                     ("C3_bf16", config_c3_bf16), ("C5", config_c5), ("C4", config_c4),
+                     ("C3_bf16", config_c3_bf16), ("C3_fullrange", config_c3_fullrange),
+                     ("C5", config_c5), ("C4", config_c4),
                      ("C4_shardG2", config_c4_shard)):
         if only and name != only:
             continue
@@ -973,11 +1164,16 @@ def _claim_stdout():
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     result_out = _claim_stdout()
     traffic, traffic_why = {}, "not collected (--no-pmc or a multi-GPU run)"
     if (not args.no_pmc and args.only is None and args.gpus == 1
             and int(os.environ.get("WORLD_SIZE", "1")) == 1):
         traffic, traffic_why = pmc_traffic(args)  # before this process initialises the GPU
+        if not args.no_configs and args.dtype == "i8" and args.synth_profile == 0:
+            # configs.C3_fullrange's own launch traffic (its inputs, score leg only)
+            _TRAFFIC_FULLRANGE.update(pmc_traffic(args, profile=1)[0])
     d = Dist(args.gpus)
     from kubernetesnetawarescheduler_amd import Engine
     eng = Engine(d.local)
@@ -1021,7 +1217,7 @@ def main():
         out["unschedulable"] = per["unschedulable"]
     if args.only not in ("vote",):
         if gpu_nodes is None:
-            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+            eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers, profile=args.synth_profile)
         cost_ms, samples = bench_cost_kernel(args, d, eng)
         nloc = N // max(d.world, args.rehearse_world)
         ops = 2.0 * P * N * nloc
@@ -1075,7 +1271,7 @@ def main():
             out["reference_mode"]["cpu_baseline"] = cpu_baseline_vote(args, eng, ref)
     if d.rank == 0 and d.world == 1 and not args.no_cpu_baseline and gpu_nodes is not None:
         # the vote path freed nothing; re-synthesise the cluster inputs (same seed)
-        eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers)
+        eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers, profile=args.synth_profile)
         out["cpu_baseline"] = cpu_baseline_place(args, eng, gpu_nodes)
     eng.close()
     if d.world == 1 and not args.no_configs and args.only is None:

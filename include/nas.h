@@ -106,6 +106,25 @@ typedef struct nas_config {
                                    * ms behind its collectives, on the stream it waits on
                                    * last (exercises NAS_OPT_COMM_TIMEOUT_MS); cleared when
                                    * used */
+#define NAS_OPT_COMMIT_WAIT_MS 5  /* bound of the device-side wait that orders a pipelined
+                                   * nas_place's last commit behind the commit stream's
+                                   * earlier ones, in ms; default 0 = automatic: the
+                                   * NAS_OPT_COMM_TIMEOUT_MS deadline when the pass issues
+                                   * collectives (10 min when that is 0), else 2000.  On
+                                   * expiry the pass fails: NAS_ERR_COMM with communicators
+                                   * aborted and the context poisoned, or NAS_ERR_HIP without
+                                   * a communicator (the context stays usable) */
+#define NAS_OPT_INJECT_COMMIT_STALL_MS 6 /* TEST ONLY, default 0: the next pipelined
+                                   * nas_place enqueues a device-side delay of this many ms
+                                   * on its commit stream ahead of the last commit there
+                                   * (exercises NAS_OPT_COMMIT_WAIT_MS); cleared when used */
+#define NAS_OPT_SYNTH_PROFILE 7 /* generator of the next nas_synth_cluster / nas_synth_batch
+                                 * (benchmarks): 0 (default) racks of 32 in zones of 16 racks,
+                                 * latency by distance class, dense background traffic 0..2
+                                 * plus bound peers in the home rack / zone; 1 SURVEY.md
+                                 * §8(d)'s C3 operand distribution over the full int8 range:
+                                 * latency U{1..127} (symmetric, zero diagonal), traffic
+                                 * U{0..127} to every node, no peer structure */
 int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value);
 
 /* per-stage device times of the last nas_place / nas_score_reference call,
@@ -126,6 +145,18 @@ typedef struct nas_timings {
 
 /* ---- lifecycle --------------------------------------------------------- */
 int nas_version(void);
+
+/* Process-wide debug counters (any thread, no context): out[i] for
+ * i < min(n, NAS_DBG_COUNT).  CU-masked streams (node-shard contexts reserve
+ * CUs for their commit stream) come from a process-wide pool: contexts borrow
+ * them and return them on nas_destroy, so CREATED stays bounded by the most
+ * masked streams ever in use at once, however many contexts come and go. */
+#define NAS_DBG_MASKED_STREAMS_CREATED 0 /* masked streams the pool ever created (all live) */
+#define NAS_DBG_MASKED_STREAMS_LENT 1    /* of them, held by contexts now */
+#define NAS_DBG_MASKED_STREAMS_IDLE 2    /* of them, idle in the pool */
+#define NAS_DBG_LIVE_CONTEXTS 3          /* contexts created and not yet destroyed */
+#define NAS_DBG_COUNT 4
+int nas_debug_counters(int64_t *out, int32_t n);
 int nas_create(nas_ctx **out, const nas_config *cfg);
 void nas_destroy(nas_ctx *ctx);
 const char *nas_last_error(nas_ctx *ctx);

@@ -28,6 +28,14 @@ NAS_OPT_STAGE_TIMINGS = 1
 NAS_OPT_COMM_TIMEOUT_MS = 2
 NAS_OPT_REHEARSE_WORLD = 3
 NAS_OPT_INJECT_STALL_MS = 4
+NAS_OPT_COMMIT_WAIT_MS = 5
+NAS_OPT_INJECT_COMMIT_STALL_MS = 6
+NAS_OPT_SYNTH_PROFILE = 7
+NAS_DBG_MASKED_STREAMS_CREATED = 0
+NAS_DBG_MASKED_STREAMS_LENT = 1
+NAS_DBG_MASKED_STREAMS_IDLE = 2
+NAS_DBG_LIVE_CONTEXTS = 3
+NAS_DBG_COUNT = 4
 K_CANDIDATES = 8
 VOTE_NOPOS = 0x7FFFFFFF
 # include/nas.h nas_vote_partial: six (value, pos1, reserved) extrema, NAS_VP_* order
@@ -71,6 +79,7 @@ _CTX = _c.c_void_p
 # name -> (restype, argtypes); mirrors include/nas.h one to one
 SIGNATURES = {
     "nas_version": (_I, []),
+    "nas_debug_counters": (_I, [_V, _I]),
     "nas_create": (_I, [_c.POINTER(_V), _c.POINTER(NasConfig)]),
     "nas_destroy": (None, [_CTX]),
     "nas_last_error": (_c.c_char_p, [_CTX]),

@@ -289,7 +289,10 @@ k_commit(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     // (nothing to do unless a walk halted), clearing the halt word
     const int h = __hip_atomic_load(halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool resume = p_begin < 0;
-    if (resume ? h < 0 : h >= 0) {  // nothing to walk (the status still goes out)
+    // (a halt word past the walk's end is not a pod: FLAG_TIMEOUT_HALT, the
+    // tail's failed wait for the commit stream -- never resumed from, and it
+    // stays for the host to report)
+    if (resume ? (h < 0 || h >= p_end) : h >= 0) {  // nothing to walk (the status still goes out)
         if (threadIdx.x == 0) status_to_stage(halt, stage_status);
         return;
     }
@@ -537,7 +540,10 @@ k_commit_w(const u64 *__restrict__ cand_key, const u64 *__restrict__ cand_bound,
     const int lane = threadIdx.x;
     const int h = __hip_atomic_load(halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool resume = p_begin < 0;
-    if (resume ? h < 0 : h >= 0) {  // nothing to walk (the status still goes out)
+    // (a halt word past the walk's end is not a pod: FLAG_TIMEOUT_HALT, the
+    // tail's failed wait for the commit stream -- never resumed from, and it
+    // stays for the host to report)
+    if (resume ? (h < 0 || h >= p_end) : h >= 0) {  // nothing to walk (the status still goes out)
         if (threadIdx.x == 0) status_to_stage(halt, stage_status);
         return;
     }

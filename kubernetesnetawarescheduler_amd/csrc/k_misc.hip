@@ -130,6 +130,19 @@ __device__ __forceinline__ int lat(unsigned long long seed, int a, int b) {
     return 40 + (int)((((hi >> 9) - (lo >> 9)) * 7) % 50) + (int)(h % 16);
 }
 
+// Profile 1 (NAS_OPT_SYNTH_PROFILE): SURVEY.md §8(d)'s C3
+// operand distribution, uniform over the whole int8 range -- latency
+// U{1..127} (the int8 form of U[1, 1000] us: ~7.9 us per step), symmetric,
+// zero diagonal; traffic U{0..127} (the int8 form of U[0, 1)) to every node,
+// no locality, no bound-peer structure
+__device__ __forceinline__ int lat_uniform(unsigned long long seed, int a, int b) {
+    if (a == b) return 0;
+    return 1 + (int)(hsh(seed, min(a, b), max(a, b), 31) % 127);
+}
+__device__ __forceinline__ int latv(unsigned long long seed, int a, int b, int profile) {
+    return profile == 1 ? lat_uniform(seed, a, b) : lat(seed, a, b);
+}
+
 template <typename T>
 __device__ __forceinline__ T from_int(int v);
 template <>
@@ -168,24 +181,37 @@ __global__ void k_synth_bg(unsigned long long seed, int N, int P, int Kp, long l
     }
 }
 
+// profile 1: uniform traffic U{0..127} to every node (zero padding past N)
 template <typename T>
-__global__ void k_synth_lt(unsigned long long seed, int N, int n0, int nloc, int Mp, int Kp,
-                           T *__restrict__ Lt) {
-    const long long total = (long long)Mp * Kp;
+__global__ void k_synth_uniform(unsigned long long seed, int N, int P, int Kp, long long total,
+                                T *__restrict__ WA) {
     for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
          t += (long long)gridDim.x * blockDim.x) {
-        const int i = (int)(t / Kp), m = (int)(t - (long long)i * Kp);
-        Lt[t] = (i < nloc && m < N) ? from_int<T>(lat(seed, m, n0 + i)) : T(0);
+        const int p = (int)(t / Kp), m = (int)(t - (long long)p * Kp);
+        const unsigned long long h = mix64(seed ^ 0x5bd1e9955bd1e995ull ^
+                                           ((unsigned long long)t * 0x9e3779b97f4a7c15ull));
+        WA[t] = from_int<T>(p < P && m < N ? (int)(h >> 57) : 0);
     }
 }
 
 template <typename T>
-__global__ void k_synth_lfull(unsigned long long seed, int N, T *__restrict__ L) {
+__global__ void k_synth_lt(unsigned long long seed, int N, int n0, int nloc, int Mp, int Kp,
+                           T *__restrict__ Lt, int profile) {
+    const long long total = (long long)Mp * Kp;
+    for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int i = (int)(t / Kp), m = (int)(t - (long long)i * Kp);
+        Lt[t] = (i < nloc && m < N) ? from_int<T>(latv(seed, m, n0 + i, profile)) : T(0);
+    }
+}
+
+template <typename T>
+__global__ void k_synth_lfull(unsigned long long seed, int N, T *__restrict__ L, int profile) {
     const long long total = (long long)N * N;
     for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < total;
          t += (long long)gridDim.x * blockDim.x) {
         const int m = (int)(t / N), n = (int)(t - (long long)m * N);
-        L[t] = from_int<T>(lat(seed, m, n));
+        L[t] = from_int<T>(latv(seed, m, n, profile));
     }
 }
 
@@ -437,21 +463,21 @@ __global__ void k_split6(const float *__restrict__ src, unsigned short *__restri
 // stores the commit's sequence number (a kernel boundary behind the commit,
 // so its capacity and status writes are released first), and the tail
 // stream's commit is preceded by a wait until the word reaches the last one.
-// The wait is bounded: after FLAG_WAIT_TICKS (2 s of the 100 MHz real-time
-// clock) it stores an impossible halt word, which the pass reports as an
-// error instead of hanging.
-constexpr unsigned long long FLAG_WAIT_TICKS = 200000000ull;
-constexpr int FLAG_TIMEOUT_HALT = 0x7ffffff0;
-
+// The wait is bounded: after `ticks` of the 100 MHz real-time clock (the
+// caller's budget: the communicator deadline when the pass issued
+// collectives, 2 s otherwise) it stores FLAG_TIMEOUT_HALT into the halt word,
+// which the pass reports as its own error (NAS_ERR_COMM, communicators
+// aborted, when collectives are involved) instead of hanging.
 __global__ void k_flag_set(unsigned long long *flag, unsigned long long v) {
     __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void k_flag_wait(const unsigned long long *flag, unsigned long long v, int *halt) {
+__global__ void k_flag_wait(const unsigned long long *flag, unsigned long long v, int *halt,
+                            unsigned long long ticks) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < v) {
-        if (__builtin_amdgcn_s_memrealtime() - t0 > FLAG_WAIT_TICKS) {
-            halt[0] = FLAG_TIMEOUT_HALT;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+            __hip_atomic_store(halt, FLAG_TIMEOUT_HALT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -465,8 +491,11 @@ hipError_t launch_flag_set(hipStream_t st, uint64_t *flag, uint64_t v) {
     return hipGetLastError();
 }
 
-hipError_t launch_flag_wait(hipStream_t st, const uint64_t *flag, uint64_t v, int32_t *halt) {
-    k_flag_wait<<<1, 1, 0, st>>>(reinterpret_cast<const unsigned long long *>(flag), v, halt);
+hipError_t launch_flag_wait(hipStream_t st, const uint64_t *flag, uint64_t v, int32_t *halt,
+                            int64_t budget_ms) {
+    // 100 MHz real-time clock: 1e5 ticks per ms
+    const unsigned long long ticks = (unsigned long long)std::max<int64_t>(budget_ms, 0) * 100000ull;
+    k_flag_wait<<<1, 1, 0, st>>>(reinterpret_cast<const unsigned long long *>(flag), v, halt, ticks);
     return hipGetLastError();
 }
 
@@ -585,24 +614,30 @@ hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int lo, 
 
 template <typename T>
 hipError_t synth_cluster_t(hipStream_t st, uint64_t seed, int N, int P, int peers, int n0, int nloc,
-                           int Mp, int Kp, int Pp, void *Lt, void *WA, int32_t *req, void *L_full) {
+                           int Mp, int Kp, int Pp, void *Lt, void *WA, int32_t *req, void *L_full,
+                           int profile) {
     hipError_t e;
     if (Lt) {
         k_synth_lt<T><<<grid_for((long long)Mp * Kp, 256), 256, 0, st>>>(seed, N, n0, nloc, Mp, Kp,
-                                                                         static_cast<T *>(Lt));
+                                                                         static_cast<T *>(Lt), profile);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (L_full) {
-        k_synth_lfull<T><<<grid_for((long long)N * N, 256), 256, 0, st>>>(seed, N,
-                                                                          static_cast<T *>(L_full));
+        k_synth_lfull<T><<<grid_for((long long)N * N, 256), 256, 0, st>>>(
+            seed, N, static_cast<T *>(L_full), profile);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (WA) {
         const long long tot = (long long)Pp * Kp;
-        k_synth_bg<T><<<grid_for(tot, 256), 256, 0, st>>>(seed, N, P, Kp, tot, static_cast<T *>(WA));
+        if (profile == 1)
+            k_synth_uniform<T><<<grid_for(tot, 256), 256, 0, st>>>(seed, N, P, Kp, tot,
+                                                                   static_cast<T *>(WA));
+        else
+            k_synth_bg<T><<<grid_for(tot, 256), 256, 0, st>>>(seed, N, P, Kp, tot, static_cast<T *>(WA));
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        k_synth_pods<T><<<(Pp + 255) / 256, 256, 0, st>>>(seed, N, P, peers, Kp, Pp,
-                                                           static_cast<T *>(WA), req);
+        // (profile 1: no bound peers -- the launch writes the requests only)
+        k_synth_pods<T><<<(Pp + 255) / 256, 256, 0, st>>>(seed, N, P, profile == 1 ? 0 : peers, Kp,
+                                                           Pp, static_cast<T *>(WA), req);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -610,15 +645,15 @@ hipError_t synth_cluster_t(hipStream_t st, uint64_t seed, int N, int P, int peer
 
 hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
                                 int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
-                                int32_t *cap, int32_t *req, void *L_full) {
+                                int32_t *cap, int32_t *req, void *L_full, int profile) {
     hipError_t e = dtype == NAS_DT_I8
                        ? synth_cluster_t<signed char>(st, seed, N, P, peers, n0, nloc, Mp, Kp, Pp,
-                                                      Lt, WA, req, L_full)
+                                                      Lt, WA, req, L_full, profile)
                    : dtype == NAS_DT_F32
                        ? synth_cluster_t<float>(st, seed, N, P, peers, n0, nloc, Mp, Kp, Pp, Lt, WA,
-                                                req, L_full)
+                                                req, L_full, profile)
                        : synth_cluster_t<unsigned short>(st, seed, N, P, peers, n0, nloc, Mp, Kp,
-                                                         Pp, Lt, WA, req, L_full);
+                                                         Pp, Lt, WA, req, L_full, profile);
     if (e != hipSuccess) return e;
     if (cap) {
         k_synth_cap<<<(N + 255) / 256, 256, 0, st>>>(seed, N, cap);

@@ -1104,8 +1104,15 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
         // 16 / 32 tiles, to shorten the commit left after the scoring,
         // measured 7-13% slower at G = 8 and 2-3% at G = 4: one more chunk
         // costs more cross-stream hops than its shorter commit saves)
+        //  the six-way split is capped at 2 x `big` tiles per chunk
+        // (~1,024 workgroups), so a much larger P keeps chunks -- and the
+        // serial merge / exchange / commit of the tail chunk after the
+        // scoring -- bounded instead of growing linearly with P; C3's plans
+        // are unchanged (G = 4: 60-tile chunks under a 104-tile cap, G = 8:
+        // 60 under 206)
         const int n = n_mt <= SHARD_CHUNKS_MAX_MT
-                          ? std::max(1, std::min(SHARD_CHUNKS - c + 1, left / 32))
+                          ? std::max({1, std::min(SHARD_CHUNKS - c + 1, left / 32),
+                                      (left + 2 * big - 1) / (2 * big)})
                           : (left + big - 1) / big;
         tiles = (left + n - 1) / n;
     }  // (decreasing chunk sizes n, n-1, ..., 1 measured 7-10% slower at G = 4 / 8)
@@ -1360,6 +1367,85 @@ void reap_comm_helpers(nas_ctx *ctx, int detach_ms = -1) {
     ctx->comm_helpers.clear();
     ctx->comm_helper_state.clear();
 }
+// Process-wide pool of CU-masked streams.  A masked
+// stream is a hardware queue of its own with the CU mask programmed into it
+// (hipExtStreamCreateWithCUMask); contexts that reserve CUs for their commit
+// stream (node shards, set_stream_masks) BORROW their masked streams from this
+// pool and give them back idle when they drop the reservation or are
+// destroyed, so a process that creates and destroys contexts keeps a bounded
+// set of masked queues -- as many as its most concurrent contexts used -- and
+// the runtime's create / destroy path for them runs once per (device, mask)
+// slot, not once per context (tools/stream_churn_probe.hip measures what
+// churning them costs).  The pool is never torn down: its streams live until
+// the process exits, like the runtime's own queue pool.
+struct MaskedPool {
+    struct Slot {
+        int dev;
+        std::vector<uint32_t> mask;
+        hipStream_t s;
+    };
+    std::mutex mu;
+    std::vector<Slot> idle;
+    int64_t created = 0, lent = 0;
+};
+MaskedPool &masked_pool() {
+    static MaskedPool *p = new MaskedPool;  // (intentionally leaked: outlives static teardown)
+    return *p;
+}
+std::atomic<int64_t> g_live_contexts{0};
+
+hipError_t masked_acquire(int dev, const std::vector<uint32_t> &mask, hipStream_t *out) {
+    MaskedPool &mp = masked_pool();
+    {
+        std::lock_guard<std::mutex> g(mp.mu);
+        for (size_t i = 0; i < mp.idle.size(); ++i)
+            if (mp.idle[i].dev == dev && mp.idle[i].mask == mask) {
+                *out = mp.idle[i].s;
+                mp.idle.erase(mp.idle.begin() + i);
+                ++mp.lent;
+                return hipSuccess;
+            }
+    }
+    const hipError_t e = hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data());
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> g(masked_pool().mu);
+    ++mp.created;
+    ++mp.lent;
+    return hipSuccess;
+}
+// s must be idle (synchronised by the caller)
+void masked_release(int dev, const std::vector<uint32_t> &mask, hipStream_t s) {
+    MaskedPool &mp = masked_pool();
+    std::lock_guard<std::mutex> g(mp.mu);
+    mp.idle.push_back({dev, mask, s});
+    --mp.lent;
+}
+// the scoring-stream and commit-stream masks of a reservation of `reserve`
+// CUs per XCD (bit i = CU i / 8 of XCD i % 8, tools/cumask_probe.hip)
+void reserve_masks(int ncu, int reserve, std::vector<uint32_t> &ms, std::vector<uint32_t> &mc) {
+    const int words = (ncu + 31) / 32;
+    ms.assign(words, 0);
+    mc.assign(words, 0);
+    for (int b = 0; b < ncu; ++b) (b < 8 * reserve ? mc : ms)[b / 32] |= 1u << (b % 32);
+}
+// give a context's streams back: masked ones to the pool, plain ones destroyed
+// (all idle); stream_x is cleared
+void drop_streams(nas_ctx *ctx) {
+    if (ctx->cu_reserve > 0) {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+        std::vector<uint32_t> ms, mc;
+        reserve_masks(ncu, ctx->cu_reserve, ms, mc);
+        masked_release(ctx->device, ms, ctx->stream);
+        masked_release(ctx->device, ms, ctx->stream2);
+        masked_release(ctx->device, mc, ctx->stream_commit);
+        if (ctx->stream_x) masked_release(ctx->device, mc, ctx->stream_x);
+    } else {
+        for (hipStream_t s : {ctx->stream, ctx->stream2, ctx->stream_commit, ctx->stream_x})
+            if (s) (void)hipStreamDestroy(s);
+    }
+    ctx->stream = ctx->stream2 = ctx->stream_commit = ctx->stream_x = nullptr;
+}
 }  // namespace
 
 extern "C" {
@@ -1391,6 +1477,22 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
         return NAS_ERR_HIP;
     }
     *out = ctx;
+    g_live_contexts.fetch_add(1);
+    return NAS_OK;
+}
+
+int nas_debug_counters(int64_t *out, int32_t n) {
+    if (!out || n < 0) return NAS_ERR_ARG;
+    MaskedPool &mp = masked_pool();
+    int64_t v[NAS_DBG_COUNT];
+    {
+        std::lock_guard<std::mutex> g(mp.mu);
+        v[NAS_DBG_MASKED_STREAMS_CREATED] = mp.created;
+        v[NAS_DBG_MASKED_STREAMS_LENT] = mp.lent;
+        v[NAS_DBG_MASKED_STREAMS_IDLE] = (int64_t)mp.idle.size();
+    }
+    v[NAS_DBG_LIVE_CONTEXTS] = g_live_contexts.load();
+    for (int i = 0; i < n && i < NAS_DBG_COUNT; ++i) out[i] = v[i];
     return NAS_OK;
 }
 
@@ -1398,6 +1500,10 @@ void nas_destroy(nas_ctx *ctx) {
     NAS_RANGE("nas_destroy");
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    // a poisoned context's communicators go first: a collective left stuck on
+    // a stream (a peer died) returns only once its communicator is aborted,
+    // and the synchronisations below would otherwise wait for it forever
+    if (ctx->poisoned) destroy_comms(ctx);
     for (hipStream_t st : {ctx->stream, ctx->stream2, ctx->stream_commit, ctx->stream_x})
         if (st) (void)hipStreamSynchronize(st);
     DevBuf *bufs[] = {&ctx->snap[0], &ctx->snap[1], &ctx->snap[2], &ctx->snap[3], &ctx->snap[4],
@@ -1412,7 +1518,8 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->g_words, &ctx->g_idx, &ctx->g_key,
                       &ctx->g_bound, &ctx->g_gk, &ctx->g_gb, &ctx->status, &ctx->scratch,
                       &ctx->vote_part, &ctx->vote_gather, &ctx->xsend[0], &ctx->xsend[1],
-                      &ctx->ovf_ptr, &ctx->ovf_m, &ctx->ovf_e, &ctx->Lr, &ctx->Lt6, &ctx->WA6};
+                      &ctx->ovf_ptr, &ctx->ovf_m, &ctx->ovf_e, &ctx->Lr, &ctx->Lt6, &ctx->WA6,
+                      &ctx->commit_flag, &ctx->zrow};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
@@ -1421,10 +1528,8 @@ void nas_destroy(nas_ctx *ctx) {
     reap_comm_helpers(ctx, 2000);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->sync_ev) (void)hipEventDestroy(ctx->sync_ev);
-    (void)hipStreamDestroy(ctx->stream);
-    (void)hipStreamDestroy(ctx->stream2);
-    (void)hipStreamDestroy(ctx->stream_commit);
-    if (ctx->stream_x) (void)hipStreamDestroy(ctx->stream_x);
+    drop_streams(ctx);  // (synchronised above; masked ones back to the pool)
+    g_live_contexts.fetch_sub(1);
     delete ctx;
 }
 
@@ -1456,6 +1561,18 @@ int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value) {
     case NAS_OPT_INJECT_STALL_MS:
         if (value < 0 || value > 60000) break;
         ctx->opt_inject_stall_ms = value;
+        return NAS_OK;
+    case NAS_OPT_COMMIT_WAIT_MS:
+        if (value < 0 || value > 3600000) break;
+        ctx->opt_commit_wait_ms = value;
+        return NAS_OK;
+    case NAS_OPT_SYNTH_PROFILE:
+        if (value < 0 || value > 1) break;
+        ctx->opt_synth_profile = (int32_t)value;
+        return NAS_OK;
+    case NAS_OPT_INJECT_COMMIT_STALL_MS:
+        if (value < 0 || value > 60000) break;
+        ctx->opt_inject_commit_stall_ms = value;
         return NAS_OK;
     default:
         return nas::fail(ctx, NAS_ERR_ARG, "nas_set_option: unknown key " + std::to_string(key));
@@ -2140,10 +2257,9 @@ int exchange_stream(nas_ctx *ctx, hipStream_t *out) {
         if (ctx->cu_reserve > 0) {
             int ncu = 0;
             HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
-            const int words = (ncu + 31) / 32;
-            std::vector<uint32_t> mc(words, 0);
-            for (int b = 0; b < 8 * ctx->cu_reserve && b < ncu; ++b) mc[b / 32] |= 1u << (b % 32);
-            e = hipExtStreamCreateWithCUMask(&ctx->stream_x, (uint32_t)words, mc.data());
+            std::vector<uint32_t> ms, mc;
+            reserve_masks(ncu, ctx->cu_reserve, ms, mc);
+            e = masked_acquire(ctx->device, mc, &ctx->stream_x);
         } else {
             int lo = 0, hi = 0;
             e = hipDeviceGetStreamPriorityRange(&lo, &hi);
@@ -2277,8 +2393,17 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // commit has run on the commit stream, else by an event (a one-chunk pass
     // with a communicator: only the pass init is on the commit stream)
     auto *cflag = ctx->commit_flag.as<uint64_t>();
+    // its bound: with collectives the communicator deadline -- the
+    // commit stream's last commit may wait on an all-gather whose peer died --
+    // so the pass fails as a communicator failure (below), never with a
+    // shorter fixed budget that makes the tail "complete" while RCCL is stuck
+    const int64_t commit_wait_ms =
+        ctx->opt_commit_wait_ms > 0 ? ctx->opt_commit_wait_ms
+        : has_coll(ctx)             ? (ctx->opt_comm_timeout_ms > 0 ? ctx->opt_comm_timeout_ms : 600000)
+                                    : 2000;
     auto after_commits = [&](hipStream_t s) -> int {
-        if (chunks.size() > 1) HIPCK(nas::launch_flag_wait(s, cflag, ctx->commit_seq, halt));
+        if (chunks.size() > 1)
+            HIPCK(nas::launch_flag_wait(s, cflag, ctx->commit_seq, halt, commit_wait_ms));
         else HIPCK(hipStreamWaitEvent(s, tm.mark(sc), 0));
         return NAS_OK;
     };
@@ -2328,7 +2453,13 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
                                  1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr,
                                  last && status_in_commit ? hs : nullptr));
         // (releases the tail chunk's commit)
-        if (!one_stream && !last) HIPCK(nas::launch_flag_set(cs, cflag, ++ctx->commit_seq));
+        if (!one_stream && !last) {
+            if (c + 2 == chunks.size() && ctx->opt_inject_commit_stall_ms > 0) {
+                (void)nas::launch_stall(cs, ctx->opt_inject_commit_stall_ms);  // (test option)
+                ctx->opt_inject_commit_stall_ms = 0;
+            }
+            HIPCK(nas::launch_flag_set(cs, cflag, ++ctx->commit_seq));
+        }
         tm.span(T_COMMIT, c0, tm.fine(cs));
         // the commit wrote this chunk's results into the pinned stage as it
         // ended, and the host unpacks them while later chunks still run.
@@ -2415,6 +2546,20 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // so only [h0, P) is unpacked again -- a bf16 C3 halt sits in the last
     // chunk, and re-unpacking all 100k pods cost ~0.25 ms of host time
     int h0 = -1;
+    if (hs[0] == nas::FLAG_TIMEOUT_HALT) {
+        // the tail commit's wait for the commit stream ran out (k_flag_wait):
+        // with collectives a peer is gone or stuck -- abort, as a missed
+        // deadline does (the stuck collective kernels return, so the streams
+        // drain and nas_destroy cannot block on them)
+        const std::string why = "the last commit's wait for the commit stream exceeded " +
+                                std::to_string(commit_wait_ms) + " ms";
+        if (has_coll(ctx)) {
+            abort_comms(ctx);
+            return nas::fail(ctx, NAS_ERR_COMM,
+                             why + " (NAS_OPT_COMM_TIMEOUT_MS): communicators aborted, context poisoned");
+        }
+        return nas::fail(ctx, NAS_ERR_HIP, why + " (NAS_OPT_COMMIT_WAIT_MS)");
+    }
     while (hs[0] >= 0) {
         // still halted after the pipeline: more gathered slots, checked in batches
         if (hs[0] >= P) return nas::fail(ctx, NAS_ERR_HIP, "commit halt word corrupt");
@@ -2644,12 +2789,11 @@ int set_stream_masks(nas_ctx *ctx, int reserve) {
         if (s) HIPCK(hipStreamSynchronize(s));
     hipStream_t ns[3] = {nullptr, nullptr, nullptr};
     hipError_t e = hipSuccess;
+    std::vector<uint32_t> ms, mc;
     if (reserve > 0) {
-        const int words = (ncu + 31) / 32;
-        std::vector<uint32_t> ms(words, 0), mc(words, 0);
-        for (int b = 0; b < ncu; ++b) (b < 8 * reserve ? mc : ms)[b / 32] |= 1u << (b % 32);
+        reserve_masks(ncu, reserve, ms, mc);
         for (int i = 0; i < 3 && e == hipSuccess; ++i)
-            e = hipExtStreamCreateWithCUMask(&ns[i], (uint32_t)words, i == 2 ? mc.data() : ms.data());
+            e = masked_acquire(ctx->device, i == 2 ? mc : ms, &ns[i]);
     } else {
         int lo = 0, hi = 0;
         e = hipDeviceGetStreamPriorityRange(&lo, &hi);
@@ -2658,16 +2802,16 @@ int set_stream_masks(nas_ctx *ctx, int reserve) {
         if (e == hipSuccess) e = hipStreamCreateWithPriority(&ns[2], hipStreamNonBlocking, hi);
     }
     if (e != hipSuccess) {
-        for (hipStream_t s : ns)
-            if (s) (void)hipStreamDestroy(s);
+        for (int i = 0; i < 3; ++i)
+            if (ns[i]) {
+                if (reserve > 0) masked_release(ctx->device, i == 2 ? mc : ms, ns[i]);
+                else (void)hipStreamDestroy(ns[i]);
+            }
         return nas::hip_fail(ctx, e, "set_stream_masks");
     }
-    (void)hipStreamDestroy(ctx->stream);
-    (void)hipStreamDestroy(ctx->stream2);
-    (void)hipStreamDestroy(ctx->stream_commit);
-    // the exchange stream is made on first use, on the commit stream's CUs
-    if (ctx->stream_x) (void)hipStreamDestroy(ctx->stream_x);
-    ctx->stream_x = nullptr;
+    // the old streams go back (masked ones to the pool); the exchange stream
+    // is made again on first use, on the commit stream's CUs
+    drop_streams(ctx);
     ctx->stream = ns[0];
     ctx->stream2 = ns[1];
     ctx->stream_commit = ns[2];
@@ -3118,6 +3262,9 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
         return nas::fail(ctx, NAS_ERR_ARG, "nas_synth_cluster arguments");
     if (B > 1 && ctx->world > 1)
         return nas::fail(ctx, NAS_ERR_UNSUPPORTED, "node shards of a cluster batch");
+    // (profile 1 has no bound peers: traffic within the int8 plane, no overflow)
+    const int profile = ctx->opt_synth_profile;
+    const int ovf_peers = profile == 1 ? 0 : peers;
     ctx->B = B;
     set_geometry(ctx, n_nodes, dtype);
     ctx->P = P;
@@ -3134,7 +3281,8 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
                                         ctx->Nloc0, ctx->Nloc, ctx->Mp, ctx->Kp, ctx->Pp,
                                         ctx->Lt.as<char>() + b * lt_b, ctx->WA.as<char>() + b * wa_b,
                                         ctx->cap0.as<int32_t>() + (size_t)b * 3 * n_nodes,
-                                        ctx->req.as<int32_t>() + (size_t)b * 3 * ctx->Pp, nullptr));
+                                        ctx->req.as<int32_t>() + (size_t)b * 3 * ctx->Pp, nullptr,
+                                        profile));
     HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)B * 3 * n_nodes * 4,
                          hipMemcpyDeviceToDevice, ctx->stream));
     HIPCK(hipStreamSynchronize(ctx->stream));
@@ -3152,7 +3300,7 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
         OK(nas::ensure(ctx, cnt, rows * 4));
         hipError_t he = hipMemsetAsync(cnt.p, 0, rows * 4, ctx->stream);
         for (int b = 0; b < B && he == hipSuccess; ++b)
-            he = nas::launch_synth_overflow(ctx->stream, seed + b, n_nodes, P, peers, ctx->Kp, 0,
+            he = nas::launch_synth_overflow(ctx->stream, seed + b, n_nodes, P, ovf_peers, ctx->Kp, 0,
                                             nullptr, cnt.as<int32_t>() + (size_t)b * ctx->Pp,
                                             nullptr, nullptr, nullptr);
         std::vector<int32_t> c(rows), ptr(rows + 1, 0);
@@ -3174,14 +3322,14 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
             HIPCK(hipMemcpyAsync(ctx->ovf_ptr.p, ptr.data(), ptr.size() * 4, hipMemcpyHostToDevice,
                                  ctx->stream));
             for (int b = 0; b < B; ++b)
-                HIPCK(nas::launch_synth_overflow(ctx->stream, seed + b, n_nodes, P, peers, ctx->Kp, 1,
+                HIPCK(nas::launch_synth_overflow(ctx->stream, seed + b, n_nodes, P, ovf_peers, ctx->Kp, 1,
                                                  nullptr, nullptr,
                                                  ctx->ovf_ptr.as<int32_t>() + (size_t)b * ctx->Pp,
                                                  ctx->ovf_m.as<int32_t>(), ctx->ovf_e.as<int32_t>()));
             HIPCK(hipStreamSynchronize(ctx->stream));
             ctx->ovf_n = tot;
         }
-        ctx->L_abs_max = 127;  // bound of the synthetic latency classes (<= 104), same on every rank
+        ctx->L_abs_max = 127;  // bound of the synthetic latency (<= 104; profile 1 <= 127), every rank
         ctx->B = B;
         OK(finish_traffic_i8(ctx));
     }
@@ -3191,6 +3339,7 @@ static int synth(nas_ctx *ctx, uint64_t seed, int32_t B, int32_t n_nodes, int32_
     ctx->L_dtype = ctx->wa_dtype = dtype;
     ctx->synth_valid = true;
     ctx->synth_seed = seed;
+    ctx->synth_profile = profile;
     return NAS_OK;
 }
 
@@ -3257,7 +3406,8 @@ int nas_read_inputs(nas_ctx *ctx, int32_t p0, int32_t np, void *WA_rows, void *L
             OK(nas::ensure(ctx, tmp, (size_t)N * N * e));
             hipError_t he = nas::launch_synth_cluster(ctx->stream, ctx->synth_seed, N, ctx->P,
                                                       ctx->dtype, 1, 0, 0, 0, 0, 0, nullptr,
-                                                      nullptr, nullptr, nullptr, tmp.p);
+                                                      nullptr, nullptr, nullptr, tmp.p,
+                                                      ctx->synth_profile);
             if (he == hipSuccess)
                 he = hipMemcpyAsync(L, tmp.p, (size_t)N * N * e, hipMemcpyDeviceToHost, ctx->stream);
             if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);

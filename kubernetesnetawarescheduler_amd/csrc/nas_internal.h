@@ -176,6 +176,7 @@ struct nas_ctx {
     bool L_finite = true;
     bool synth_valid = false;   // inputs came from nas_synth_cluster(synth_seed)
     uint64_t synth_seed = 0;
+    int32_t synth_profile = 0;  // the profile the synthetic inputs were generated with
 
     // ---- multi-GPU
     ncclComm *comm = nullptr;    // scoring chunks on `stream` and host-side rescores
@@ -208,6 +209,9 @@ struct nas_ctx {
     int64_t opt_comm_timeout_ms = 120000;
     int32_t opt_rehearse_world = 0;
     int64_t opt_inject_stall_ms = 0;
+    int64_t opt_commit_wait_ms = 0;         // 0: automatic (NAS_OPT_COMMIT_WAIT_MS)
+    int64_t opt_inject_commit_stall_ms = 0;
+    int32_t opt_synth_profile = 0;          // NAS_OPT_SYNTH_PROFILE
     bool poisoned = false;       // a collective missed its deadline: communicators aborted
     // timing events, created once and reused by every call (hipEventCreate
     // per mark cost a small placement more than its kernels)
@@ -319,10 +323,13 @@ hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t
 // = 0; cap_snap[0, n) = cap[0, n) when cap_snap is non-null
 // the commit order across the commit stream and the tail chunk's stream
 // (k_misc.hip): flag_set stores v into *flag behind the stream's work so far,
-// flag_wait holds the stream until *flag >= v (bounded; on timeout it writes
-// an impossible halt word, reported as an error by the pass)
+// flag_wait holds the stream until *flag >= v, for at most budget_ms; on
+// timeout it writes FLAG_TIMEOUT_HALT into *halt (an impossible halt word:
+// halts are pod indices), which the pass reports as its own error
+constexpr int32_t FLAG_TIMEOUT_HALT = 0x7ffffff0;
 hipError_t launch_flag_set(hipStream_t st, uint64_t *flag, uint64_t v);
-hipError_t launch_flag_wait(hipStream_t st, const uint64_t *flag, uint64_t v, int32_t *halt);
+hipError_t launch_flag_wait(hipStream_t st, const uint64_t *flag, uint64_t v, int32_t *halt,
+                            int64_t budget_ms);
 hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
                             int n);
 // rehearsal: rank slots 1..G-1 of an all-gathered buffer [G][n] of keys
@@ -367,7 +374,8 @@ hipError_t launch_synth_snapshots(hipStream_t st, uint64_t seed, int n, int lo, 
                                   int64_t *rx, int64_t *tx, int64_t *disk);
 hipError_t launch_synth_cluster(hipStream_t st, uint64_t seed, int N, int P, int dtype, int peers,
                                 int n0, int nloc, int Mp, int Kp, int Pp, void *Lt, void *WA,
-                                int32_t *cap, int32_t *req, void *L_full /* optional N*N */);
+                                int32_t *cap, int32_t *req, void *L_full /* optional N*N */,
+                                int profile /* NAS_OPT_SYNTH_PROFILE */);
 // int8 synthetic traffic is exact: pass 0 writes the plane and ovf_cnt[p] (the
 // entries of pod p outside [-128, 127]); pass 1 (after the host's prefix sum
 // into ovf_ptr) writes the entries.  Peer aggregates are recomputed from the

@@ -19,6 +19,19 @@ _FDT = {"cpu": np.float64, "mem": np.float64, "rx": np.int64, "tx": np.int64,
         "bw": np.float64, "disk": np.int64}
 
 
+def debug_counters():
+    """nas_debug_counters: process-wide {masked_streams_created, _lent, _idle,
+    live_contexts} (include/nas.h NAS_DBG_*)."""
+    out = np.zeros(_lib.NAS_DBG_COUNT, np.int64)
+    rc = _lib.lib().nas_debug_counters(ptr(out), _lib.NAS_DBG_COUNT)
+    if rc != 0:
+        raise NasError(rc, "nas_debug_counters")
+    return {"masked_streams_created": int(out[_lib.NAS_DBG_MASKED_STREAMS_CREATED]),
+            "masked_streams_lent": int(out[_lib.NAS_DBG_MASKED_STREAMS_LENT]),
+            "masked_streams_idle": int(out[_lib.NAS_DBG_MASKED_STREAMS_IDLE]),
+            "live_contexts": int(out[_lib.NAS_DBG_LIVE_CONTEXTS])}
+
+
 class LocalGroup:
     """nas_local_group: `world` Engines of this process that exchange like
     RCCL ranks.  Each rank's calls must run on their own thread (ctypes
@@ -275,7 +288,8 @@ class Engine:
         self._ck(self._L.nas_set_batch(self._h, n_clusters))
         self.n_clusters = n_clusters
 
-    def synth_batch(self, seed, n_clusters, n_nodes, P, dtype="i8", peers=8):
+    def synth_batch(self, seed, n_clusters, n_nodes, P, dtype="i8", peers=8, profile=0):
+        self.set_option("SYNTH_PROFILE", profile)
         self._ck(self._L.nas_synth_batch(self._h, seed, n_clusters, n_nodes, P, self._dt(dtype),
                                          peers))
         self.n_clusters, self.n_nodes, self.n_pods, self.dtype = n_clusters, n_nodes, P, dtype
@@ -396,7 +410,10 @@ class Engine:
             ci = None if ci is None else ci.reshape(B, P)
         return node, cf, ci
 
-    def synth_cluster(self, seed, n_nodes, P, dtype="i8", peers=8):
+    def synth_cluster(self, seed, n_nodes, P, dtype="i8", peers=8, profile=0):
+        """nas_synth_cluster; profile (NAS_OPT_SYNTH_PROFILE): 0 racks / zones
+        with bound peers, 1 uniform over the full int8 range."""
+        self.set_option("SYNTH_PROFILE", profile)
         self._ck(self._L.nas_synth_cluster(self._h, seed, n_nodes, P, self._dt(dtype), peers))
         self.n_nodes, self.n_pods, self.dtype = n_nodes, P, dtype
 

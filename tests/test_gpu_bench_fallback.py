@@ -35,3 +35,28 @@ def test_bench_rccl_failure_falls_back_to_host_exchange(tmp_path):
     assert out["n_gpus"] == 2
     assert out["config"]["exchange"].startswith("host gloo all-gather")
     assert out["value"] > 0 and out["unschedulable"] == 0
+
+
+def test_bench_self_launch_two_ranks_on_one_gpu(tmp_path):
+    """`python bench.py --gpus 2` with no launcher: bench.py
+    starts both rank processes itself (file:// rendezvous, LOCAL_RANK wrapped
+    over the visible GPUs), both land on GPU 0 here, RCCL refuses, the ranks
+    agree on the host exchange, and the parent relays rank 0's one line."""
+    args = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+            "--nodes", "1500", "--pods", "4096", "--steps", "2", "--warmup", "1", "--no-configs",
+            "--no-reference-mode", "--no-cpu-baseline", "--no-pmc"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "NAS_DIST_INIT")}
+    out_f, err_f = tmp_path / "stdout", tmp_path / "stderr"
+    import subprocess
+    with open(out_f, "w") as fo, open(err_f, "w") as fe:
+        r = subprocess.run(args, env=env, cwd=ROOT, stdout=fo, stderr=fe, timeout=160)
+    out_txt, err_txt = out_f.read_text(), err_f.read_text()
+    assert r.returncode == 0, err_txt[-3000:]
+    lines = [ln for ln in out_txt.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), out_txt[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert "self-launch" in out["config"]["launcher"]
+    assert out["config"]["exchange"].startswith("host gloo all-gather")
+    assert out["value"] > 0 and out["unschedulable"] == 0

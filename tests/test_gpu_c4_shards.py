@@ -1,6 +1,8 @@
 """BASELINE config C4 (50k nodes x 500k pods, node axis split over 2/4/8
-GPUs) at its own size, split into G = 2 and G = 4 VIRTUAL node shards on one
-GPU.
+GPUs) at its own size, split into G = 2, 4 and 8 VIRTUAL node shards on one
+GPU (G = 8, the 6,250-column shard geometry, VERDICT r5
+item 7: eight contexts each holding the replicated 25 GB traffic matrix,
+~27 GB per context of the 288 GB).
 
 Each shard is its own context (nas_set_shard(r, G) before the uploads) that
 scores only node columns [r*N/G, (r+1)*N/G) over the full 50k-deep K; the
@@ -35,7 +37,7 @@ def world1():
     return node, score, free, cap0, req
 
 
-@pytest.mark.parametrize("G", [2, 4])
+@pytest.mark.parametrize("G", [2, 4, 8])
 def test_c4_virtual_shards_equal_world1(world1, G):
     node1, score1, free1, cap0, req = world1
     engines = []

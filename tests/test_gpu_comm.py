@@ -120,3 +120,67 @@ def test_comm_init_with_the_system_rccl():
                        timeout=100)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "/opt/rocm" in r.stdout, r.stdout
+
+
+# the tail commit's bounded wait for the commit stream
+# (k_flag_wait) -- its budget, and how its expiry is reported.  The stall is
+# injected on the commit stream ahead of its last flag store
+# (NAS_OPT_INJECT_COMMIT_STALL_MS); 30,000 pods over 2,000 nodes is a
+# three-chunk pass, so the tail chunk waits for the commit stream.
+def _three_chunk_cluster(e):
+    e.synth_cluster(11, 2000, 30000, "i8", peers=8)
+
+
+def test_commit_wait_timeout_without_comm_is_an_error_not_a_hang():
+    with Engine(0) as e:
+        _three_chunk_cluster(e)
+        want, _, wscore = e.place()
+        e.set_option("COMMIT_WAIT_MS", 100)
+        e.set_option("INJECT_COMMIT_STALL_MS", 1500)
+        e.reset_capacity()
+        with pytest.raises(NasError) as ei:
+            e.place()
+        assert ei.value.code == _lib.NAS_ERR_HIP
+        assert "NAS_OPT_COMMIT_WAIT_MS" in str(ei.value) and "100 ms" in str(ei.value)
+        # not poisoned: the next pass (the stall is used up) is the same as before
+        e.set_option("COMMIT_WAIT_MS", 0)
+        e.reset_capacity()
+        node, _, score = e.place()
+        assert (node == want).all() and (score == wscore).all()
+
+
+def test_commit_wait_timeout_with_comm_aborts_and_poisons():
+    with Engine(0) as e:
+        e.comm_init(Engine.comm_unique_id(), 0, 1)
+        _three_chunk_cluster(e)
+        e.place()
+        # the host's own deadline is far away: the device-side wait expires first
+        e.set_option("COMM_TIMEOUT_MS", 20000)
+        e.set_option("COMMIT_WAIT_MS", 100)
+        e.set_option("INJECT_COMMIT_STALL_MS", 1500)
+        e.reset_capacity()
+        t0 = time.monotonic()
+        with pytest.raises(NasError) as ei:
+            e.place()
+        assert ei.value.code == _lib.NAS_ERR_COMM
+        assert "communicators aborted" in str(ei.value)
+        assert time.monotonic() - t0 < 15
+        with pytest.raises(NasError) as ei:
+            e.reset_capacity()
+        assert ei.value.code == _lib.NAS_ERR_COMM
+    # (nas_destroy of the poisoned context returned: the aborted communicators
+    # are torn down before its streams are synchronised)
+
+
+def test_commit_wait_budget_defaults_to_comm_deadline():
+    """With a communicator the wait takes NAS_OPT_COMM_TIMEOUT_MS, so a stall
+    shorter than that deadline (but longer than the old fixed 2 s) passes."""
+    with Engine(0) as e:
+        e.comm_init(Engine.comm_unique_id(), 0, 1)
+        _three_chunk_cluster(e)
+        want, _, _ = e.place()
+        e.set_option("COMM_TIMEOUT_MS", 8000)
+        e.set_option("INJECT_COMMIT_STALL_MS", 2500)
+        e.reset_capacity()
+        node, _, _ = e.place()
+        assert (node == want).all()

@@ -17,8 +17,10 @@ pytestmark = pytest.mark.gpu
 N, P, SEED = 10000, 100000, 0x4E4153
 
 
-def test_c3_fullsize_properties(engine):
-    engine.synth_cluster(SEED, N, P, "i8", peers=8)
+@pytest.mark.parametrize("profile", [0, 1])
+def test_c3_fullsize_properties(engine, profile):
+    # profile 1: SURVEY.md §8(d)'s full-range operands (configs.C3_fullrange)
+    engine.synth_cluster(SEED, N, P, "i8", peers=8, profile=profile)
     engine.reset_capacity()
     node, _, score = engine.place()
     _, L, cap0, req = engine.read_inputs(0, 0, want_L=True)
