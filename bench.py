@@ -65,6 +65,9 @@ def parse():
                     help="diagnostic at --gpus 1: time rank 0 of a G-GPU node-sharded pass "
                          "(its node columns; the other ranks' lists are shifted copies of its "
                          "own; placements not meaningful, RCCL over a one-rank communicator)")
+    ap.add_argument("--commit-cus", type=int, default=None,
+                    help="NAS_OPT_COMMIT_CUS for the headline pass (world 1): CUs per XCD kept "
+                         "for the commit stream (default: the engine's)")
     ap.add_argument("--synth-profile", type=int, default=0, choices=[0, 1],
                     help="generator of the C3 inputs (NAS_OPT_SYNTH_PROFILE): 0 racks / zones "
                          "with bound peers (default), 1 uniform over the full int8 range "
@@ -404,6 +407,8 @@ def bench_place(args, d, eng):
             return bench_place_host(args, d, eng) + (eng, exchange)
     else:
         eng.synth_cluster(SEED, N, P, args.dtype, peers=args.peers, profile=args.synth_profile)
+    if args.commit_cus is not None:
+        eng.set_option("COMMIT_CUS", args.commit_cus)
     keys = ("cost_ms", "fit_ms", "merge_ms", "commit_ms", "total_ms", "cost_launches",
             "rescore_rounds", "unschedulable")
     acc = dict.fromkeys(keys, 0.0)

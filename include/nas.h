@@ -125,6 +125,20 @@ typedef struct nas_config {
                                  * §8(d)'s C3 operand distribution over the full int8 range:
                                  * latency U{1..127} (symmetric, zero diagonal), traffic
                                  * U{0..127} to every node, no peer structure */
+#define NAS_OPT_COMMIT_CUS 8     /* CUs per XCD kept for the commit stream of a world-1
+                                  * context's nas_place (0..4, default 0: none); the scoring
+                                  * streams then run on the other CUs (CU-masked streams from
+                                  * the process-wide pool).  Node shards keep their own
+                                  * reservation (nas_comm_init). */
+#define NAS_OPT_COST_CACHE 9      /* cost-row cache of nas_place (one cluster): the pass's
+                                   * cost launches also store every (pod, node) cost, P x N
+                                   * x 4 B (4 GB at 10k x 100k), and its gathered rescores
+                                   * read a pod's row instead of recomputing the contraction
+                                   * (herds: every pod ranking the same nodes first).
+                                   * 0 off, 1 on, 2 (default) auto: on when the previous
+                                   * nas_place of the same shape needed >= 4 rescore rounds
+                                   * and the cache takes <= 16 GB.  Placements are the same
+                                   * either way. */
 int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value);
 
 /* per-stage device times of the last nas_place / nas_score_reference call,

@@ -145,28 +145,6 @@ __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
     return d;
 }
 
-// Per-lane running top-4 as separate (orderable cost, node) u32 words.
-// A lane visits its nodes in ascending node order, so a new (x, n) sorts
-// before entry j iff x < cost[j] strictly (an equal cost has the larger node):
-// four independent 32-bit compares and a select network, no 64-bit compares.
-struct Top4 {
-    unsigned c[4], n[4];
-    __device__ __forceinline__ void init() {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c[j] = n[j] = 0xffffffffu;
-    }
-    __device__ __forceinline__ void insert(unsigned x, unsigned node) {
-        const bool b0 = x < c[0], b1 = x < c[1], b2 = x < c[2], b3 = x < c[3];
-        const unsigned c3 = b2 ? c[2] : (b3 ? x : c[3]), n3 = b2 ? n[2] : (b3 ? node : n[3]);
-        const unsigned c2 = b1 ? c[1] : (b2 ? x : c[2]), n2 = b1 ? n[1] : (b2 ? node : n[2]);
-        const unsigned c1 = b0 ? c[0] : (b1 ? x : c[1]), n1 = b0 ? n[0] : (b1 ? node : n[1]);
-        c[0] = b0 ? x : c[0];
-        n[0] = b0 ? node : n[0];
-        c[1] = c1; n[1] = n1; c[2] = c2; n[2] = n2; c[3] = c3; n[3] = n3;
-    }
-    __device__ __forceinline__ u64 key(int j) const { return ((u64)c[j] << 32) | n[j]; }
-};
-
 // Instantiations (launch_cost_t): NWN = 4 (256 x 256) with the k_fit mask
 // (node shards, rescore windows), with the fused fit (FUSE: main pod ranges at
 // world 1, batches) or with a row map (RMAP); NWN = 6 (the wide tile, always
@@ -181,7 +159,7 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
             int n_mt, int n_nt, int p0, int Pp, const u64 *__restrict__ mask,
             u64 *__restrict__ partial, u64 *__restrict__ pbound, int node_base,
             const int *__restrict__ dyn_start, int dyn_hi, const int *__restrict__ dyn_hi_ptr,
-            Ovf ov, const int *__restrict__ rowmap, FitSrc fs) {
+            Ovf ov, const int *__restrict__ rowmap, FitSrc fs, unsigned *__restrict__ cc) {
     static_assert(NWN == 4 || NWN == 6, "the 8- and 12-wave layouts");
     constexpr int NW = 2 * NWN;              // waves
     constexpr int NI = 2;                    // 32-pod columns per wave
@@ -616,6 +594,33 @@ k_cost_topk(const unsigned char *__restrict__ Lt, const unsigned char *__restric
         fr = l & (PB - 1);
         fh = l / PB;
     }
+    if (cc) {
+        // the cost-row cache (gathered rescores of a herd read it instead of
+        // recomputing the contraction, k_rescore.hip k_rescore_cached): every
+        // (pod, local node) value as its orderable 32-bit key, row-major
+        // [cluster][Pp][Mp]; a lane's four consecutive nodes per 16-byte
+        // store, and the lanes of one pod (l, l ^ 32; 16x16 also l ^ 16,
+        // l ^ 48) fill whole 128-byte lines of its row between them, which
+        // the L2 combines before they go to HBM
+        unsigned *crow = cc + (size_t)cb * Pp * (n_mt * BM) + mt * BM + wm * 128;
+#pragma unroll
+        for (int ni = 0; ni < AN; ++ni) {
+            const int pod = p0 + nt * BNK + wn * WPODS + ni * PB + fr;
+            if (pod >= p_end) continue;
+            unsigned *d = crow + (size_t)pod * (n_mt * BM);
+#pragma unroll
+            for (int mi = 0; mi < AM; ++mi)
+#pragma unroll
+                for (int g = 0; g < AR / 4; ++g) {
+                    uint4 v;
+                    v.x = M::okey(acc[mi][ni][4 * g + 0]);
+                    v.y = M::okey(acc[mi][ni][4 * g + 1]);
+                    v.z = M::okey(acc[mi][ni][4 * g + 2]);
+                    v.w = M::okey(acc[mi][ni][4 * g + 3]);
+                    *reinterpret_cast<uint4 *>(d + (M16 ? mi * 16 + 4 * fh : mi * 32 + 8 * g + 4 * fh)) = v;
+                }
+        }
+    }
     if constexpr (FUSE) {
         // the fused fit, after the main loop: nothing of it is live across
         // the loop (held there, its registers pushed the loop's LDS-DMA
@@ -932,7 +937,8 @@ template <int DT, bool RMAP, int NWN = 4, bool FUSE = (NWN == 6)>
 hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp, int Kb, int Pp,
                          int p0, int np, const uint64_t *mask, uint64_t *partial,
                          uint64_t *pbound, int node_base, const Dyn *dyn, int batch,
-                         const Ovf &ov, const int32_t *rowmap, const FitSrc &fs = FitSrc{}) {
+                         const Ovf &ov, const int32_t *rowmap, const FitSrc &fs = FitSrc{},
+                         uint32_t *cache = nullptr) {
     constexpr int BNK = NWN * 64;
     constexpr bool WIDE = BNK > BN;
     const void *fn = reinterpret_cast<const void *>(&k_cost_topk<DT, RMAP, NWN, FUSE>);
@@ -959,7 +965,8 @@ hipError_t launch_cost_t(hipStream_t st, const void *Lt, const void *WA, int Mp,
     // the wide tile's launch end rides in dyn_hi (unused without a window)
     const int dhi = WIDE ? p0 + np : dh;
     k_cost_topk<DT, RMAP, NWN, FUSE><<<dim3(n_mt * n_nt, batch), 128 * NWN, lds, st>>>(
-        lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dhi, dhp, ov, rowmap, fs);
+        lt, wa, Kb, n_mt, n_nt, p0, Pp, mk, pa, pb, node_base, ds, dhi, dhp, ov, rowmap, fs,
+        reinterpret_cast<unsigned *>(cache));
     return hipGetLastError();
 }
 
@@ -973,8 +980,9 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
                             int Kp, int Pp, int p0, int np, const uint64_t *mask,
                             uint64_t *partial, uint64_t *pbound, int node_base, const Dyn *dyn,
                             int batch, const Ovf *ovf, const int32_t *rowmap, bool wide,
-                            const FitSrc *fit) {
+                            const FitSrc *fit, uint32_t *cache) {
     if (fit && (dyn || rowmap)) return hipErrorInvalidValue;  // windows keep the k_fit mask
+    if (cache && (dyn || rowmap)) return hipErrorInvalidValue;  // the cache: main pod ranges
     if (!fit && wide && !dyn && !rowmap) return hipErrorInvalidValue;  // the wide tile fuses
     const Ovf ov = ovf ? *ovf : Ovf{};
     if (rowmap && (!dyn || batch != 1)) return hipErrorInvalidValue;
@@ -983,12 +991,13 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
                                        node_base, dyn, batch, OVV, rowmap)                        \
      : (!dyn && wide)                                                                             \
             ? launch_cost_t<DTV, false, 6>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound, \
-                                           node_base, dyn, batch, OVV, nullptr, *fit)             \
+                                           node_base, dyn, batch, OVV, nullptr, *fit, cache)      \
      : fit ? launch_cost_t<DTV, false, 4, true>(st, Lt, WA, Mp, KB, Pp, p0, np,     \
                                                              mask, partial, pbound, node_base,    \
-                                                             dyn, batch, OVV, nullptr, *fit)      \
+                                                             dyn, batch, OVV, nullptr, *fit,      \
+                                                             cache)                               \
             : launch_cost_t<DTV, false>(st, Lt, WA, Mp, KB, Pp, p0, np, mask, partial, pbound,    \
-                                        node_base, dyn, batch, OVV, nullptr))
+                                        node_base, dyn, batch, OVV, nullptr, FitSrc{}, cache))
     if (dyn) {  // tiles covering any window [s, s + win) clipped to hi: one extra for the offset
         p0 = 0;
         np = (int)round_up(dyn->win, BN) + BN;

@@ -125,7 +125,90 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
     }
 }
 
+// Cost-row cache rescoring (round 6).  In a global herd -- every pod ranks
+// the same nodes first (configs.C3_fullrange: uniform random latency, so a
+// node's column sum dominates every pod's cost) -- most pods' lists, scored
+// against capacity a few thousand pods stale, run dry at their turn, and the
+// walk rescored ~90% of C3's pods through gathered slots whose cost launch
+// recomputes the whole contraction (a workgroup's full-K loop, ~150 us per
+// slot).  When the pass keeps the cost-row cache (the main cost launches
+// store every (pod, node) key, k_cost.hip), a slot's pods are rescored from
+// their cached rows instead: one wave per view row reads the pod's Mp keys
+// (coalesced), tests each node's fit against the capacity now (exactly
+// k_fit's rule), keeps a per-lane top-4 in ascending node order (klist.h
+// Top4) and merges the 64 lanes' lists by xor shuffles into the pod's 8-list
+// with its exactness bound -- the list the fit + cost + merge kernels would
+// have produced, for a read of 4 B per (pod, node) instead of 2 K MACs.
+// Output: the view rows (to_view: [R][8] keys, [R] bounds, for the node-shard
+// exchange) or straight into the pods' own list slots (row q -> pod idx[q]).
+constexpr int RC_THREADS = 256;
+__global__ void __launch_bounds__(RC_THREADS)
+k_rescore_cached(const unsigned *__restrict__ cc, int stride, int nloc, int n0,
+                 const int *__restrict__ cap, int N, const int *__restrict__ req, int Pp,
+                 const int *__restrict__ idx, const int *__restrict__ ctl,
+                 u64 *__restrict__ key_out, u64 *__restrict__ bound_out, int to_view) {
+    const int q = blockIdx.x * (RC_THREADS / 64) + (int)(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (ctl[0] < 0 || q >= ctl[1]) return;  // (wave-uniform) nothing halted / past the view
+    const int p = idx[q];
+    const int r0 = req[p], r1 = req[Pp + p], r2 = req[2 * Pp + p];
+    const unsigned *row = cc + (size_t)p * stride;
+    const int *c0 = cap + n0, *c1 = cap + N + n0, *c2 = cap + 2 * N + n0;
+    Top4 t;
+    t.init();
+    int i = lane;
+    // four nodes per lane in flight per iteration (ascending per lane)
+    for (; i + 192 < nloc; i += 256) {
+        unsigned x[4];
+        bool f[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = i + 64 * u;
+            x[u] = row[j];
+            f[u] = r0 <= c0[j] && r1 <= c1[j] && r2 <= c2[j];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t.insert(f[u] ? x[u] : 0xffffffffu, (unsigned)(n0 + i + 64 * u));
+    }
+    for (; i < nloc; i += 64) {
+        const unsigned x = row[i];
+        const bool f = r0 <= c0[i] && r1 <= c1[i] && r2 <= c2[i];
+        t.insert(f ? x : 0xffffffffu, (unsigned)(n0 + i));
+    }
+    u64 k4[4], o4[4], kl[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) k4[j] = t.c[j] == 0xffffffffu ? KEY_INVALID : t.key(j);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o4[j] = shfl_xor64(k4[j], 1);
+    merge44(k4, o4, kl);
+    u64 bl = umin64(k4[3], o4[3]);
+#pragma unroll
+    for (int m = 2; m < 64; m <<= 1) {
+        u64 o8[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o8[j] = shfl_xor64(kl[j], m);
+        bl = umin64(bl, shfl_xor64(bl, m));
+        merge88(kl, o8);
+    }
+    bl = umin64(bl, kl[7]);
+    if (lane != 0) return;
+    const size_t r = to_view ? (size_t)q : (size_t)p;
+    store8(key_out + r * KC, kl);
+    bound_out[r] = bl;
+}
+
 }  // namespace
+
+hipError_t launch_rescore_cached(hipStream_t st, const uint32_t *cache, int stride, int nloc,
+                                 int n0, const int32_t *cap, int N, const int32_t *req, int Pp,
+                                 const int32_t *idx, const int32_t *ctl, int R, uint64_t *key_out,
+                                 uint64_t *bound_out, bool to_view) {
+    if (R <= 0) return hipSuccess;
+    k_rescore_cached<<<(R + RC_THREADS / 64 - 1) / (RC_THREADS / 64), RC_THREADS, 0, st>>>(
+        reinterpret_cast<const unsigned *>(cache), stride, nloc, n0, cap, N, req, Pp, idx, ctl,
+        reinterpret_cast<u64 *>(key_out), reinterpret_cast<u64 *>(bound_out), to_view ? 1 : 0);
+    return hipGetLastError();
+}
 
 int stale_words(int P) { return (P + STALE_THREADS - 1) / STALE_THREADS * (STALE_THREADS / 64); }
 

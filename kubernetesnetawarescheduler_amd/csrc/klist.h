@@ -51,6 +51,29 @@ __device__ __forceinline__ u64 shfl_xor64(u64 x, int m) {
     return ((u64)(unsigned)hi << 32) | (unsigned)lo;
 }
 
+// Per-lane running top-4 as separate (orderable cost, node) u32 words.
+// A lane visits its nodes in ascending node order, so a new (x, n) sorts
+// before entry j iff x < cost[j] strictly (an equal cost has the larger node):
+// four independent 32-bit compares and a select network, no 64-bit compares.
+// (cost all-ones is never inserted: the "does not fit" value of the callers)
+struct Top4 {
+    unsigned c[4], n[4];
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[j] = n[j] = 0xffffffffu;
+    }
+    __device__ __forceinline__ void insert(unsigned x, unsigned node) {
+        const bool b0 = x < c[0], b1 = x < c[1], b2 = x < c[2], b3 = x < c[3];
+        const unsigned c3 = b2 ? c[2] : (b3 ? x : c[3]), n3 = b2 ? n[2] : (b3 ? node : n[3]);
+        const unsigned c2 = b1 ? c[1] : (b2 ? x : c[2]), n2 = b1 ? n[1] : (b2 ? node : n[2]);
+        const unsigned c1 = b0 ? c[0] : (b1 ? x : c[1]), n1 = b0 ? n[0] : (b1 ? node : n[1]);
+        c[0] = b0 ? x : c[0];
+        n[0] = b0 ? node : n[0];
+        c[1] = c1; n[1] = n1; c[2] = c2; n[2] = n2; c[3] = c3; n[3] = n3;
+    }
+    __device__ __forceinline__ u64 key(int j) const { return ((u64)c[j] << 32) | n[j]; }
+};
+
 __device__ __forceinline__ void load8(const u64 *p, u64 (&k)[8]) {
     const ulonglong2 *s = reinterpret_cast<const ulonglong2 *>(p);
 #pragma unroll

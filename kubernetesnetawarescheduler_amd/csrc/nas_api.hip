@@ -87,15 +87,29 @@ constexpr int RESCORE_PODS = 1024;  // pods per device-side rescore slot (multip
 // first 1024 of them always let the walk finish -- the slot's cost launch
 // 690 -> 235 us, the halting pass's slots 0.9 -> 0.37 ms (traced); 256 / 512
 // need more slots (profiles/r04_ab_gather_pods.txt)
+// (round 6: 6 tiles = 1,536 pods for C3 -- still one wave of cost workgroups
+// over 40 node tiles -- took 65 instead of 89 slots through the full-range
+// herd but 31.6 instead of 29.4 ms, same box: profiles/r06b_ab_slots.txt)
 constexpr int GATHER_PODS = 1024;
+// a pass with the cost-row cache rescores from cached rows (k_rescore_cached:
+// no cost launch), so its slots take more pods
+constexpr int GATHER_PODS_CACHED = 2048;
+// NAS_OPT_COST_CACHE auto: the previous pass's rescore rounds that turn the
+// cache on, and its largest size (C4 at world 1 would need 100 GB)
+constexpr int CACHE_MIN_ROUNDS = 4;
+constexpr size_t CACHE_MAX_BYTES = (size_t)16 << 30;
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
 constexpr int MAX_SPEC_SLOTS = 8;         // speculative slots at most (nas_place, slot_hint)
 // ... except the second check: a walk still halted after a full batch is
 // usually nearly done (C2: 5 slots), and an idle slot's ~8 launches cost about
 // what one more host round trip does, so the second batch is one slot (C2
 // median 1.17 / 1.07 / 1.04 ms with a second batch of 4 / 2 / 1, same
-// placements)
-int gather_batch(int check) { return check == 2 ? 1 : GATHER_SLOTS_PER_SYNC; }
+// placements).  With the cost-row cache (a herd; an idle slot is 3 launches)
+// 8 slots per check from the fourth on
+int gather_batch(int check, bool cached) {
+    return check == 2 ? 1 : (cached && check > 3) ? 8 : GATHER_SLOTS_PER_SYNC;
+}
+int plan_n_mt(const nas_ctx *ctx);
 // (a one-slot FIRST batch for walks halting near their end helped a 12-pod
 // rescore, 0.39 -> 0.26 ms, but cost bench C1's 3-slot case two extra round
 // trips, 0.39 -> 0.52 ms: with a round trip ~2 idle slots, 4 then 1 is the
@@ -361,16 +375,16 @@ int tile_pods(const nas_ctx *ctx) {
 hipError_t launch_cost(nas_ctx *ctx, hipStream_t st, int Pp, int p0, int np, const uint64_t *mask,
                        const nas::Dyn *dyn, int batch, const nas::Ovf *ov,
                        const int32_t *rowmap = nullptr, const nas::FitSrc *fit = nullptr,
-                       bool narrow = false) {
+                       bool narrow = false, uint32_t *cache = nullptr) {
     const bool wide = !narrow && wide_ok(ctx);
     if (ctx->dtype == NAS_DT_F32)
         return nas::launch_cost_topk(st, NAS_DT_BF16, ctx->Lt6.p, ctx->WA6.p, ctx->Mp, 6 * ctx->Kp,
                                      Pp, p0, np, mask, ctx->partial.as<uint64_t>(),
                                      ctx->pbound.as<uint64_t>(), ctx->Nloc0, dyn, batch, nullptr,
-                                     rowmap, wide, fit);
+                                     rowmap, wide, fit, cache);
     return nas::launch_cost_topk(st, ctx->dtype, ctx->Lt.p, ctx->WA.p, ctx->Mp, ctx->Kp, Pp, p0, np,
                                  mask, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(),
-                                 ctx->Nloc0, dyn, batch, ov, rowmap, wide, fit);
+                                 ctx->Nloc0, dyn, batch, ov, rowmap, wide, fit, cache);
 }
 
 // exact traffic row (n values, each within int32) -> the int8 plane row and
@@ -390,6 +404,7 @@ void split_row(const int64_t *v, int n, signed char *plane, std::vector<int32_t>
 
 // the call issued collectives other ranks must join (waits get deadlines)
 bool has_coll(const nas_ctx *ctx) { return ctx->comm != nullptr || ctx->local != nullptr; }
+int set_stream_masks(nas_ctx *ctx, int reserve);  // (multi-GPU section)
 
 int check_extended(nas_ctx *ctx) {
     if (!ctx->have_L || !ctx->have_cap || !ctx->have_pods || !ctx->have_wa)
@@ -727,7 +742,10 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
                               p_lo, p_hi - p_lo, mask));
     hipEvent_t e1 = fuse ? e0 : tm.fine(st);
     const nas::Ovf ov = make_ovf(ctx);
-    HIPCK(launch_cost(ctx, st, v.Pp, pr0, np, mask, nullptr, 1, &ov, nullptr, fuse ? &fit : nullptr));
+    // (a pass with the cost-row cache: the main launches store every cost too)
+    uint32_t *cache = ctx->cache_active && !view ? ctx->cost_cache.as<uint32_t>() : nullptr;
+    HIPCK(launch_cost(ctx, st, v.Pp, pr0, np, mask, nullptr, 1, &ov, nullptr, fuse ? &fit : nullptr,
+                      false, cache));
     hipEvent_t e2 = tm.fine(st);
     tm.span(T_FIT, e0, e1);
     tm.span(T_COST, e1, e2);
@@ -738,7 +756,7 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
 
 // Gathered rescore slot, all on the device (k_rescore.hip): if the commit walk
 // has halted (halt word >= 0), every pending pod in [halt, hi) whose list is
-// dry against the capacity now -- up to GATHER_PODS of them, in pod order, the
+// dry against the capacity now -- up to R of them (GATHER_PODS), in pod order, the
 // halted pod first -- is copied into a scratch view, scored there by the
 // ordinary fit / cost / merge kernels (+ the exchange across ranks), its list
 // written back, and the walk resumed from the halt.  Nothing halted: every
@@ -746,7 +764,7 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
 // collectives).  Slots need no host round trip, so a crowded cluster's many
 // stops cost launches, not synchronisations.
 int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, int ch, int32_t *pub, int hi) {
-    const int R = std::min(GATHER_PODS, ctx->Pp);
+    const int R = std::min(ctx->cache_active ? GATHER_PODS_CACHED : GATHER_PODS, ctx->Pp);
     OK(nas::ensure(ctx, ctx->g_words, (size_t)nas::stale_words(ctx->Pp) * 8));
     OK(nas::ensure(ctx, ctx->g_idx, (size_t)R * 4));
     OK(nas::ensure(ctx, ctx->g_key, (size_t)R * KC * 8));
@@ -760,6 +778,39 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, int ch, int32_t *pub,
     HIPCK(nas::launch_stale_scan(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                  ctx->req.as<int32_t>(), ctx->Pp, ctx->cap.as<int32_t>(), ctx->N,
                                  -1, hi, ctx->g_words.as<uint64_t>(), R, idx, ctl, halt));
+    const bool xch = exchanging(ctx);
+    auto *ck = ctx->cand_key.as<uint64_t>();
+    auto *cbnd = ctx->cand_bound.as<uint64_t>();
+    if (ctx->cache_active) {
+        // the pods' costs are in the cost-row cache: each view row's list from
+        // its cached row against the capacity now (k_rescore_cached), straight
+        // into the pod's own slot -- or into the view rows for the exchange
+        hipEvent_t e1 = tm.fine(st);
+        HIPCK(nas::launch_rescore_cached(st, ctx->cost_cache.as<uint32_t>(), ctx->Mp, ctx->Nloc,
+                                         ctx->Nloc0, ctx->cap.as<int32_t>(), ctx->N,
+                                         ctx->req.as<int32_t>(), ctx->Pp, idx, ctl, R,
+                                         xch ? gk : ck, xch ? gb : cbnd, xch));
+        hipEvent_t e3 = tm.fine(st);
+        nas::Dyn dyn{ctl, R, 0, ctl + 1};
+        if (xch) {
+            OK(nas::ensure(ctx, ctx->g_gk, (size_t)ctx->world * R * KC * 8));
+            OK(nas::ensure(ctx, ctx->g_gb, (size_t)ctx->world * R * 8));
+            auto *xk = ctx->g_gk.as<uint64_t>();
+            auto *xb = ctx->g_gb.as<uint64_t>();
+            OK(exchange(ctx, ch, st, gk, gb, (size_t)R, xk, xb));
+            HIPCK(nas::launch_merge(st, xk, xb, ctx->world, (int64_t)R * KC, R, 0, 0, 0, ck, cbnd, 0,
+                                    &dyn, 0, 1, 0, idx));
+        }
+        hipEvent_t e4 = tm.fine(st);
+        HIPCK(nas::launch_commit(st, ck, cbnd, ctx->req.as<int32_t>(), ctx->Pp, -1, hi,
+                                 ctx->cap.as<int32_t>(), ctx->N, ctx->out_node.as<int32_t>(),
+                                 ctx->out_cost_i.as<int32_t>(), halt, 1, pub, zrow_ptr(ctx)));
+        tm.span(T_COST, e1, e3);
+        tm.span(T_MERGE, e3, e4);
+        tm.span(T_COMMIT, e0, e1);
+        tm.span(T_COMMIT, e4, tm.fine(st));
+        return NAS_OK;
+    }
     nas::Dyn dyn{ctl, R, 0, ctl + 1};
     auto *mask = ctx->mask.as<uint64_t>();
     hipEvent_t e1 = tm.fine(st);
@@ -772,9 +823,6 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, int ch, int32_t *pub,
     const int n_lists = ctx->Mp / nas::COST_BM;
     // the last merge writes the fresh lists straight into the pods' own list
     // slots (idx); with an exchange, the local merge first fills the view
-    const bool xch = exchanging(ctx);
-    auto *ck = ctx->cand_key.as<uint64_t>();
-    auto *cbnd = ctx->cand_bound.as<uint64_t>();
     HIPCK(nas::launch_merge(st, ctx->partial.as<uint64_t>(), ctx->pbound.as<uint64_t>(), n_lists,
                             (int64_t)R * KC, R, 0, 0, 0, xch ? gk : ck, xch ? gb : cbnd, 0, &dyn,
                             0, 1, 0, xch ? nullptr : idx));
@@ -1464,6 +1512,9 @@ int nas_create(nas_ctx **out, const nas_config *cfg) {
     nas_ctx *ctx = new (std::nothrow) nas_ctx();
     if (!ctx) return NAS_ERR_NOMEM;
     ctx->device = dev;
+    if (hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ctx->n_cu <= 0)
+        ctx->n_cu = 256;
     // the commit stream runs at the highest priority: its one-workgroup walks
     // and rescore slots take the next CU a scoring workgroup frees instead of
     // queueing behind a whole scoring launch
@@ -1519,7 +1570,7 @@ void nas_destroy(nas_ctx *ctx) {
                       &ctx->g_bound, &ctx->g_gk, &ctx->g_gb, &ctx->status, &ctx->scratch,
                       &ctx->vote_part, &ctx->vote_gather, &ctx->xsend[0], &ctx->xsend[1],
                       &ctx->ovf_ptr, &ctx->ovf_m, &ctx->ovf_e, &ctx->Lr, &ctx->Lt6, &ctx->WA6,
-                      &ctx->commit_flag, &ctx->zrow};
+                      &ctx->commit_flag, &ctx->zrow, &ctx->cost_cache};
     for (DevBuf *b : bufs)
         if (b->p) (void)hipFree(b->p);
     if (ctx->host_status.p) (void)hipHostFree(ctx->host_status.p);
@@ -1565,6 +1616,14 @@ int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value) {
     case NAS_OPT_COMMIT_WAIT_MS:
         if (value < 0 || value > 3600000) break;
         ctx->opt_commit_wait_ms = value;
+        return NAS_OK;
+    case NAS_OPT_COST_CACHE:
+        if (value < 0 || value > 2) break;
+        ctx->opt_cost_cache = (int32_t)value;
+        return NAS_OK;
+    case NAS_OPT_COMMIT_CUS:
+        if (value < 0 || value > 4) break;
+        ctx->opt_commit_cus = (int32_t)value;
         return NAS_OK;
     case NAS_OPT_SYNTH_PROFILE:
         if (value < 0 || value > 1) break;
@@ -2283,6 +2342,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         return nas::fail(ctx, NAS_ERR_STATE,
                          "nas_place on a shard needs nas_comm_init (nas_set_shard scores only)");
     if (!node_out) return nas::fail(ctx, NAS_ERR_ARG, "node_out null");
+    // world 1: the commit stream's own CUs (NAS_OPT_COMMIT_CUS), so chunk
+    // merges and commits run as chunks land instead of queueing behind the
+    // wide cost workgroups (node shards set theirs in nas_comm_init)
+    if (ctx->world == 1 && !has_coll(ctx) && ctx->cu_reserve != ctx->opt_commit_cus)
+        OK(set_stream_masks(ctx, ctx->opt_commit_cus));
     OK(alloc_extended(ctx));
     OK(prepare_ovf(ctx));
     OK(prepare_split(ctx));
@@ -2293,6 +2357,25 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     hipStream_t st = ctx->stream, sc = ctx->stream_commit;
     const int P = ctx->P, N = ctx->N;
     int32_t *halt = ctx->status.as<int32_t>();
+    // The cost-row cache (NAS_OPT_COST_CACHE, k_rescore_cached): in auto mode
+    // when the previous pass of this shape needed CACHE_MIN_ROUNDS rescore
+    // rounds or more (a herd: consecutive passes over similar clusters stop
+    // alike, as the speculative slots below assume too).  It costs the main
+    // cost launches a 4-byte store per (pod, node) and saves every gathered
+    // slot its fit / cost / merge launches.  Same placements either way.
+    struct CacheOff {
+        nas_ctx *c;
+        ~CacheOff() { c->cache_active = false; }
+    } cache_off{ctx};
+    ctx->cache_active = false;
+    if (ctx->opt_cost_cache != 0) {
+        const bool herd = ctx->slot_hint_P == P && ctx->slot_hint_N == N &&
+                          ctx->last_rescore_rounds >= CACHE_MIN_ROUNDS;
+        const size_t bytes = (size_t)ctx->Pp * ctx->Mp * 4;
+        if ((ctx->opt_cost_cache == 1 || herd) && bytes <= CACHE_MAX_BYTES)
+            ctx->cache_active = nas::ensure(ctx, ctx->cost_cache, bytes) == NAS_OK;
+        if (!ctx->cache_active) ctx->err.clear();  // (no memory: the slots recompute)
+    }
     hipEvent_t t0 = tm.mark(st);
     // Each chunk is filtered against the working capacity as the commit
     // stream has left it so far: every value read is >= the capacity at the
@@ -2567,7 +2650,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         // (with speculative slots the walk may have resumed and halted again:
         // its first halt is status word 3)
         if (h0 < 0) h0 = spec > 0 ? (hs[1] > 0 ? std::min(std::max(hs[3], 0), hs[0]) : hs[0]) : hs[0];
-        for (int r = 0, n = gather_batch(checks); r < n; ++r)
+        for (int r = 0, n = gather_batch(checks, ctx->cache_active); r < n; ++r)
             OK(gathered_slot(ctx, tm, st, CH_SCORE, nullptr, P));
         OK(fetch());
         if (hs[0] < 0) {
@@ -2587,6 +2670,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     ctx->timings.unschedulable = unsched;
     ctx->timings.commit_rounds = hs[2];
     ctx->slot_hint = std::min(hs[1], MAX_SPEC_SLOTS);
+    ctx->last_rescore_rounds = hs[1];
     ctx->slot_hint_P = P;
     ctx->slot_hint_N = N;
     ctx->scored = true;

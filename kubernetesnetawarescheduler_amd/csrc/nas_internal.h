@@ -92,6 +92,7 @@ struct CommInit;    // nas_api.hip: state shared with a nas_comm_init helper thr
 
 struct nas_ctx {
     int device = 0;
+    int n_cu = 256;                    // compute units of the device
     hipStream_t stream = nullptr;      // main stream (uploads, scoring, results)
     hipStream_t stream2 = nullptr;     // second scoring stream (chunk tails overlap)
     hipStream_t stream_commit = nullptr;  // commit walks, pipelined behind scoring
@@ -114,6 +115,11 @@ struct nas_ctx {
     // gathered slots the previous nas_place of shape (P, N) needed: enqueued
     // speculatively by the next pass of that shape
     int32_t slot_hint = 0, slot_hint_P = -1, slot_hint_N = -1;
+    int32_t last_rescore_rounds = 0;  // of the previous nas_place of shape (slot_hint_P, _N)
+    // cost-row cache (NAS_OPT_COST_CACHE): [Pp][Mp] orderable keys of the
+    // current pass's main cost launches, read by its gathered rescore slots
+    nas::DevBuf cost_cache;
+    bool cache_active = false;
     // NAS_DT_F32: the operands as six-segment bf16 splits (prepare_split);
     // the fp32 Lt / WA stay for read-back and host-side updates
     nas::DevBuf Lt6, WA6;
@@ -212,6 +218,8 @@ struct nas_ctx {
     int64_t opt_commit_wait_ms = 0;         // 0: automatic (NAS_OPT_COMMIT_WAIT_MS)
     int64_t opt_inject_commit_stall_ms = 0;
     int32_t opt_synth_profile = 0;          // NAS_OPT_SYNTH_PROFILE
+    int32_t opt_commit_cus = 0;             // NAS_OPT_COMMIT_CUS (world 1)
+    int32_t opt_cost_cache = 2;             // NAS_OPT_COST_CACHE: 0 off, 1 on, 2 auto
     bool poisoned = false;       // a collective missed its deadline: communicators aborted
     // timing events, created once and reused by every call (hipEventCreate
     // per mark cost a small placement more than its kernels)
@@ -285,7 +293,10 @@ hipError_t launch_cost_topk(hipStream_t st, int dtype, const void *Lt, const voi
                             uint64_t *partial, uint64_t *pbound, int node_base,
                             const Dyn *dyn = nullptr, int batch = 1, const Ovf *ovf = nullptr,
                             const int32_t *rowmap = nullptr, bool wide = false,
-                            const FitSrc *fit = nullptr);
+                            const FitSrc *fit = nullptr, uint32_t *cache = nullptr);
+// cache (main pod ranges only): every (pod, local node) cost of the launch as
+// its orderable 32-bit key into cache[cluster][Pp][Mp] (the cost-row cache,
+// rescored from by launch_rescore_cached)
 hipError_t launch_merge(hipStream_t st, const uint64_t *keys, const uint64_t *bounds, int n_lists,
                         int64_t stride, int64_t bstride, int src_p0, int p0, int np,
                         uint64_t *cand_key, uint64_t *cand_bound, int dst_p0 = 0,
@@ -318,6 +329,15 @@ hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t
                              const int32_t *req, int Pp, const int32_t *cap, int N, int p0, int P,
                              uint64_t *words, int R, int32_t *idx, int32_t *ctl,
                              const int32_t *p0_dev = nullptr);
+
+// rescore from the cost-row cache (cache[Pp][stride], this rank's nloc local
+// nodes from global node n0): view row q < ctl[1] (nothing if ctl[0] < 0) is
+// pod idx[q]; its 8-list + bound against the capacity now go to view row q
+// (to_view) or to the pod's own slot p of key_out / bound_out
+hipError_t launch_rescore_cached(hipStream_t st, const uint32_t *cache, int stride, int nloc,
+                                 int n0, const int32_t *cap, int N, const int32_t *req, int Pp,
+                                 const int32_t *idx, const int32_t *ctl, int R, uint64_t *key_out,
+                                 uint64_t *bound_out, bool to_view);
 
 // start of a nas_place pass: status[0] = -1 (halt), status[1 .. 2*STATUS_INTS)
 // = 0; cap_snap[0, n) = cap[0, n) when cap_snap is non-null

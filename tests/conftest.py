@@ -19,3 +19,21 @@ def engine():
     e = Engine(0)
     yield e
     e.close()
+
+
+# NAS_TEST_COMMIT_CUS=k (test runs only): every Engine the suite creates keeps
+# k CUs per XCD for its commit stream (NAS_OPT_COMMIT_CUS) -- the round-5
+# "rw2" configuration (CU-masked streams on EVERY context) whose suite run hung
+# in the ~50th nas_create; with the process-wide masked-stream pool the whole
+# suite must run green this way
+_COMMIT_CUS = int(os.environ.get("NAS_TEST_COMMIT_CUS", "0") or 0)
+if _COMMIT_CUS:
+    from kubernetesnetawarescheduler_amd import engine as _engine_mod
+
+    _orig_init = _engine_mod.Engine.__init__
+
+    def _init_with_commit_cus(self, *a, **k):
+        _orig_init(self, *a, **k)
+        self.set_option("COMMIT_CUS", _COMMIT_CUS)
+
+    _engine_mod.Engine.__init__ = _init_with_commit_cus
