@@ -139,6 +139,15 @@ typedef struct nas_config {
                                    * nas_place of the same shape needed >= 4 rescore rounds
                                    * and the cache takes <= 16 GB.  Placements are the same
                                    * either way. */
+#define NAS_OPT_HERD_PLAN 10      /* nas_place's chunk plan (one cluster, no communicator):
+                                   * 0 pipelined (chunks scored on two streams while the
+                                   * commit stream walks earlier ones; each chunk's fit sees
+                                   * the capacity two or more chunks back), 1 the herd plan
+                                   * (fit + cost, merge and commit chunk after chunk on one
+                                   * stream: every chunk's fit sees its predecessors'
+                                   * commits), 2 (default) auto: pipelined until a pass of
+                                   * the shape needs >= 8 rescore rounds, then the herd plan
+                                   * for that shape.  Placements are the same either way. */
 int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value);
 
 /* per-stage device times of the last nas_place / nas_score_reference call,

@@ -33,6 +33,7 @@ NAS_OPT_INJECT_COMMIT_STALL_MS = 6
 NAS_OPT_SYNTH_PROFILE = 7
 NAS_OPT_COMMIT_CUS = 8
 NAS_OPT_COST_CACHE = 9
+NAS_OPT_HERD_PLAN = 10
 NAS_DBG_MASKED_STREAMS_CREATED = 0
 NAS_DBG_MASKED_STREAMS_LENT = 1
 NAS_DBG_MASKED_STREAMS_IDLE = 2

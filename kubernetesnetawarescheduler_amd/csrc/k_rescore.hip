@@ -141,40 +141,50 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
 // have produced, for a read of 4 B per (pod, node) instead of 2 K MACs.
 // Output: the view rows (to_view: [R][8] keys, [R] bounds, for the node-shard
 // exchange) or straight into the pods' own list slots (row q -> pod idx[q]).
-constexpr int RC_THREADS = 256;
+constexpr int RC_THREADS = 256;  // one workgroup (4 waves) per view row
+constexpr int RC_UNROLL = 8;     // nodes per thread in flight (cost + 3 capacities each)
 __global__ void __launch_bounds__(RC_THREADS)
 k_rescore_cached(const unsigned *__restrict__ cc, int stride, int nloc, int n0,
                  const int *__restrict__ cap, int N, const int *__restrict__ req, int Pp,
                  const int *__restrict__ idx, const int *__restrict__ ctl,
                  u64 *__restrict__ key_out, u64 *__restrict__ bound_out, int to_view) {
-    const int q = blockIdx.x * (RC_THREADS / 64) + (int)(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (ctl[0] < 0 || q >= ctl[1]) return;  // (wave-uniform) nothing halted / past the view
+    __shared__ u64 xl[RC_THREADS / 64][KC + 1];
+    const int q = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (ctl[0] < 0 || q >= ctl[1]) return;  // (block-uniform) nothing halted / past the view
     const int p = idx[q];
     const int r0 = req[p], r1 = req[Pp + p], r2 = req[2 * Pp + p];
     const unsigned *row = cc + (size_t)p * stride;
     const int *c0 = cap + n0, *c1 = cap + N + n0, *c2 = cap + 2 * N + n0;
+    // thread t visits nodes t, t + 256, ... (ascending: Top4's tie rule);
+    // RC_UNROLL of them per round trip -- the walk is latency-bound otherwise
+    // (one wave per row with 4 in flight ran 146 us per 2,048-row slot)
     Top4 t;
     t.init();
-    int i = lane;
-    // four nodes per lane in flight per iteration (ascending per lane)
-    for (; i + 192 < nloc; i += 256) {
-        unsigned x[4];
-        bool f[4];
+    int i = tid;
+    for (; i + (RC_UNROLL - 1) * RC_THREADS < nloc; i += RC_UNROLL * RC_THREADS) {
+        unsigned x[RC_UNROLL];
+        int a[RC_UNROLL], b[RC_UNROLL], c[RC_UNROLL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int j = i + 64 * u;
+        for (int u = 0; u < RC_UNROLL; ++u) {
+            const int j = i + RC_THREADS * u;
             x[u] = row[j];
-            f[u] = r0 <= c0[j] && r1 <= c1[j] && r2 <= c2[j];
+            a[u] = c0[j];
+            b[u] = c1[j];
+            c[u] = c2[j];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) t.insert(f[u] ? x[u] : 0xffffffffu, (unsigned)(n0 + i + 64 * u));
+        for (int u = 0; u < RC_UNROLL; ++u)
+            t.insert((r0 <= a[u] && r1 <= b[u] && r2 <= c[u]) ? x[u] : 0xffffffffu,
+                     (unsigned)(n0 + i + RC_THREADS * u));
     }
-    for (; i < nloc; i += 64) {
+    for (; i < nloc; i += RC_THREADS) {
         const unsigned x = row[i];
         const bool f = r0 <= c0[i] && r1 <= c1[i] && r2 <= c2[i];
         t.insert(f ? x : 0xffffffffu, (unsigned)(n0 + i));
     }
+    // the wave's 64 lists -> one 8-list + bound (xor shuffles), then the
+    // four waves' lists through LDS
     u64 k4[4], o4[4], kl[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) k4[j] = t.c[j] == 0xffffffffu ? KEY_INVALID : t.key(j);
@@ -190,8 +200,22 @@ k_rescore_cached(const unsigned *__restrict__ cc, int stride, int nloc, int n0,
         bl = umin64(bl, shfl_xor64(bl, m));
         merge88(kl, o8);
     }
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < KC; ++j) xl[w][j] = kl[j];
+        xl[w][KC] = bl;
+    }
+    __syncthreads();
+    if (tid != 0) return;
+#pragma unroll
+    for (int v = 1; v < RC_THREADS / 64; ++v) {
+        u64 o8[8];
+#pragma unroll
+        for (int j = 0; j < KC; ++j) o8[j] = xl[v][j];
+        bl = umin64(bl, xl[v][KC]);
+        merge88(kl, o8);
+    }
     bl = umin64(bl, kl[7]);
-    if (lane != 0) return;
     const size_t r = to_view ? (size_t)q : (size_t)p;
     store8(key_out + r * KC, kl);
     bound_out[r] = bl;
@@ -204,7 +228,7 @@ hipError_t launch_rescore_cached(hipStream_t st, const uint32_t *cache, int stri
                                  const int32_t *idx, const int32_t *ctl, int R, uint64_t *key_out,
                                  uint64_t *bound_out, bool to_view) {
     if (R <= 0) return hipSuccess;
-    k_rescore_cached<<<(R + RC_THREADS / 64 - 1) / (RC_THREADS / 64), RC_THREADS, 0, st>>>(
+    k_rescore_cached<<<R, RC_THREADS, 0, st>>>(
         reinterpret_cast<const unsigned *>(cache), stride, nloc, n0, cap, N, req, Pp, idx, ctl,
         reinterpret_cast<u64 *>(key_out), reinterpret_cast<u64 *>(bound_out), to_view ? 1 : 0);
     return hipGetLastError();

@@ -98,6 +98,10 @@ constexpr int GATHER_PODS_CACHED = 2048;
 // cache on, and its largest size (C4 at world 1 would need 100 GB)
 constexpr int CACHE_MIN_ROUNDS = 4;
 constexpr size_t CACHE_MAX_BYTES = (size_t)16 << 30;
+// NAS_OPT_HERD_PLAN auto: rescore rounds of one pass that make its shape a herd
+constexpr int HERD_MIN_ROUNDS = 8;
+// gathered slots behind each chunk's commit in the herd plan
+constexpr int HERD_SLOTS = 3;
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
 constexpr int MAX_SPEC_SLOTS = 8;         // speculative slots at most (nas_place, slot_hint)
 // ... except the second check: a walk still halted after a full batch is
@@ -1186,10 +1190,22 @@ int chunk_pods(const nas_ctx *ctx, int c, int lo) {
 // chunk first (chunks then finish in pod order) measured the same or 0.5%
 // slower, and so did moving units from a stream's short last chunk to its
 // previous one (r03_ab_chunk_order.txt).
-std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx) {
+std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx, bool herd = false) {
     std::vector<std::pair<int, int>> chunks;
     const int P = ctx->P;
     const bool wide = tile_pods(ctx) != nas::COST_BN && ctx->world == 1;
+    if (herd) {
+        // the herd plan's chunks, one after another on one stream: ~1.25 pods
+        // per node each (a chunk's own pods compete for the nodes its fit saw
+        // free; tools/herd_model.py), at most 48 units (C3: 32 wide tiles =
+        // 1,280 workgroups over 40 node tiles, whole waves), whole cost tiles
+        const int unit = tile_pods(ctx) / std::gcd(tile_pods(ctx), nas::COST_BN);
+        int units = (int)std::min<int64_t>(CHUNK_TILES_WIDE, (5LL * ctx->N / 4 + nas::COST_BN - 1) / nas::COST_BN);
+        units = std::max(unit, (units + unit - 1) / unit * unit);
+        const int step = units * nas::COST_BN;
+        for (int lo = 0; lo < P; lo += step) chunks.push_back({lo, std::min(P, lo + step)});
+        return chunks;
+    }
     if (!wide) {
         for (int c = 0, lo = 0; lo < P; ++c) {
             const int hi = std::min(P, lo + chunk_pods(ctx, c, lo));
@@ -1616,6 +1632,10 @@ int nas_set_option(nas_ctx *ctx, int32_t key, int64_t value) {
     case NAS_OPT_COMMIT_WAIT_MS:
         if (value < 0 || value > 3600000) break;
         ctx->opt_commit_wait_ms = value;
+        return NAS_OK;
+    case NAS_OPT_HERD_PLAN:
+        if (value < 0 || value > 2) break;
+        ctx->opt_herd_plan = (int32_t)value;
         return NAS_OK;
     case NAS_OPT_COST_CACHE:
         if (value < 0 || value > 2) break;
@@ -2376,6 +2396,11 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
             ctx->cache_active = nas::ensure(ctx, ctx->cost_cache, bytes) == NAS_OK;
         if (!ctx->cache_active) ctx->err.clear();  // (no memory: the slots recompute)
     }
+    // the herd plan (NAS_OPT_HERD_PLAN; below): auto = sticky for a shape
+    // once one of its passes needed HERD_MIN_ROUNDS rescore rounds
+    const bool herd = !has_coll(ctx) &&
+                      (ctx->opt_herd_plan == 1 ||
+                       (ctx->opt_herd_plan == 2 && ctx->herd_P == P && ctx->herd_N == N));
     hipEvent_t t0 = tm.mark(st);
     // Each chunk is filtered against the working capacity as the commit
     // stream has left it so far: every value read is >= the capacity at the
@@ -2407,7 +2432,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // chunk bounds; every scoring launch is enqueued before any commit-stream
     // work, so the host's enqueue time of merges / commits / copies never
     // delays the next chunk's cost launch
-    const std::vector<std::pair<int, int>> chunks = plan_chunks(ctx);
+    const std::vector<std::pair<int, int>> chunks = plan_chunks(ctx, herd);
     // a one-chunk pass without a communicator has nothing to pipeline: its
     // merge / commit / copies stay on the scoring stream, which saves the
     // cross-stream event hops (~15-20 us each) that dominate a small pass
@@ -2428,54 +2453,16 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     // they leave 2-3 CUs per XCD to the commit stream, profiles/r04_ab_reserve.txt;
     // round 3's masks that reserved 8-16 CUs beside the narrow tile measured
     // 25-35% slower, r03_ab_reserve_cus.txt)
-    const hipStream_t ss2[2] = {st, ctx->stream2};
-    if (!one_stream) {
-        hipEvent_t ready = tm.mark(st);
-        for (hipStream_t s : {ss2[0], ss2[1], sc})
-            if (s != st) HIPCK(hipStreamWaitEvent(s, ready, 0));
-    }
-    std::vector<hipEvent_t> scored(chunks.size());
-    // fit + cost only on the two scoring streams (a chunk's tail blocks overlap
-    // the next chunk; a third scoring stream measured 5% slower at G = 1 and
-    // 6-25% at G = 8); the commit stream merges (and exchanges, over its own
-    // communicator) each chunk right before committing it, so no cost launch
-    // ever waits behind a merge or an all-gather
-    for (size_t c = 0; c < chunks.size(); ++c) {
-        hipStream_t ss = ss2[c & 1];
-        OK(score_range(ctx, tm, chunks[c].first, chunks[c].second, ss, score_cap, nullptr, false));
-        // (one stream: nothing waits on it -- every event record or wait is a
-        // packet the queue processes between two kernels)
-        scored[c] = one_stream ? nullptr : tm.mark(ss);
-    }
-    // (one stream: the chunk's merge starts the status words itself)
-    const bool init_in_merge = one_stream && live_cap;
-    if (live_cap && !init_in_merge) OK(pass_init(sc));
-    // speculative slots: as many as the previous pass of this shape needed
-    // (consecutive passes over similar clusters stop alike), enqueued before
-    // the first status round trip; a slot whose walk is not halted exits at
-    // once.  Not with a communicator: every rank must issue the same slots.
-    const int spec = (!has_coll(ctx) && ctx->slot_hint_P == P && ctx->slot_hint_N == N) ? ctx->slot_hint : 0;
+    const int spec = (!herd && !has_coll(ctx) && ctx->slot_hint_P == P && ctx->slot_hint_N == N)
+                         ? ctx->slot_hint : 0;
+    // (the herd plan's slots run inside its chunk loop, behind each commit;
+    // pods they place after their chunk's rows were staged are unpacked again
+    // at the end, like the speculative slots' -- `late_slots`)
+    const bool late_slots = spec > 0 || herd;
     // (an injected stall, NAS_OPT_INJECT_STALL_MS, sits on st behind the
     // pass: the host must wait on st then)
     // (the pass's last commit writes the status words to the pinned host area)
-    const bool status_in_commit = spec == 0 && ctx->opt_inject_stall_ms == 0;
-    // A node-shard pass's chunks merge and exchange on their own stream (sx,
-    // the commit stream's communicator and CUs) and the commit stream only
-    // commits, each commit waiting for its chunk's merged lists: with every
-    // chunk's merge -> all-gather -> merge -> commit chain on the commit
-    // stream the chains of the last two chunks ran back to back after the
-    // scoring (~108 us each at G = 8 with six shard chunks); now one chunk's
-    // exchange overlaps the previous chunk's commit.  The tail chunk merges
-    // and exchanges on its scoring stream right behind its cost launch (its
-    // stream's own communicator and gather buffers, so the collectives of
-    // each communicator stay on one stream in one order) and commits there
-    // after the commit stream's last commit.
-    const bool xs_mode = exchanging(ctx) && !one_stream;
-    // the tail chunk's stream waits for the commit stream's last commit: by
-    // the device word behind each commit (launch_flag_set / flag_wait) once a
-    // commit has run on the commit stream, else by an event (a one-chunk pass
-    // with a communicator: only the pass init is on the commit stream)
-    auto *cflag = ctx->commit_flag.as<uint64_t>();
+    const bool status_in_commit = !late_slots && ctx->opt_inject_stall_ms == 0;
     // its bound: with collectives the communicator deadline -- the
     // commit stream's last commit may wait on an all-gather whose peer died --
     // so the pass fails as a communicator failure (below), never with a
@@ -2484,90 +2471,167 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         ctx->opt_commit_wait_ms > 0 ? ctx->opt_commit_wait_ms
         : has_coll(ctx)             ? (ctx->opt_comm_timeout_ms > 0 ? ctx->opt_comm_timeout_ms : 600000)
                                     : 2000;
-    auto after_commits = [&](hipStream_t s) -> int {
-        if (chunks.size() > 1)
-            HIPCK(nas::launch_flag_wait(s, cflag, ctx->commit_seq, halt, commit_wait_ms));
-        else HIPCK(hipStreamWaitEvent(s, tm.mark(sc), 0));
-        return NAS_OK;
-    };
-    hipStream_t sx = nullptr;
-    if (xs_mode) OK(exchange_stream(ctx, &sx));
-    for (size_t c = 0; c < chunks.size(); ++c) {
-        const int lo = chunks[c].first, hi = chunks[c].second;
-        // the last chunk is merged and committed on its own scoring stream
-        // behind the commit stream's earlier work (long finished by then), so
-        // the pass's serial tail after the last cost launch has no
-        // cross-stream hop in front of its merge (the communicator is the
-        // commit stream's: its collectives stay in one order)
-        const bool tail = !one_stream && c + 1 == chunks.size();
-        const bool last = c + 1 == chunks.size();
-        hipStream_t cs = sc;
-        if (xs_mode) {
-            if (tail) {
-                cs = ss2[c & 1];
-                OK(merge_range(ctx, tm, lo, hi, cs, (c & 1) ? CH_SCORE2 : CH_SCORE, (int)(c & 1),
-                               main_view(ctx)));
-                OK(after_commits(cs));
+    if (herd) {
+        // The herd plan: chunk after chunk on one stream -- fit + cost, merge,
+        // commit -- so every chunk's fused fit reads the capacity its
+        // predecessors' commits left (lag 1) instead of a capacity two or
+        // more chunks stale.  In a global herd (configs.C3_fullrange: every
+        // pod ranks the same nodes first) the pipelined plan's stale lists
+        // run dry for most pods and the walk rescored ~90% of them in ~90
+        // gathered slots; a CPU model of the walk (tools/herd_model.py,
+        // profiles/r06e_herd_model.txt) needs 15 slots at lag 2, 1 at lag 1.  The
+        // cost is the scoring / commit overlap: each chunk's merge and commit
+        // run with the GPU otherwise idle.
+        if (live_cap) OK(pass_init(st));
+        for (size_t c = 0; c < chunks.size(); ++c) {
+            const int lo = chunks[c].first, hi = chunks[c].second;
+            const bool last = c + 1 == chunks.size();
+            OK(score_range(ctx, tm, lo, hi, st, score_cap, nullptr, false));
+            OK(merge_range(ctx, tm, lo, hi, st, CH_SCORE, 0, main_view(ctx)));
+            hipEvent_t c0 = tm.fine(st);
+            HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                                     ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(),
+                                     N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
+                                     halt, 1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr,
+                                     last && status_in_commit ? hs : nullptr));
+            tm.span(T_COMMIT, c0, tm.fine(st));
+            // a walk halted in this chunk resumes here, before the next chunk
+            // is scored against the capacity it leaves: HERD_SLOTS gathered
+            // slots over the pods scored so far (hi), each a few idle launches
+            // when nothing halted; a halt they leave is resumed by the next
+            // chunk's slots or the host loop below
+            for (int r = 0; r < HERD_SLOTS; ++r) OK(gathered_slot(ctx, tm, st, CH_SCORE, pub, hi));
+            landed.push_back({lo, hi, tm.mark(st)});
+        }
+    } else {
+        const hipStream_t ss2[2] = {st, ctx->stream2};
+        if (!one_stream) {
+            hipEvent_t ready = tm.mark(st);
+            for (hipStream_t s : {ss2[0], ss2[1], sc})
+                if (s != st) HIPCK(hipStreamWaitEvent(s, ready, 0));
+        }
+        std::vector<hipEvent_t> scored(chunks.size());
+        // fit + cost only on the two scoring streams (a chunk's tail blocks overlap
+        // the next chunk; a third scoring stream measured 5% slower at G = 1 and
+        // 6-25% at G = 8); the commit stream merges (and exchanges, over its own
+        // communicator) each chunk right before committing it, so no cost launch
+        // ever waits behind a merge or an all-gather
+        for (size_t c = 0; c < chunks.size(); ++c) {
+            hipStream_t ss = ss2[c & 1];
+            OK(score_range(ctx, tm, chunks[c].first, chunks[c].second, ss, score_cap, nullptr, false));
+            // (one stream: nothing waits on it -- every event record or wait is a
+            // packet the queue processes between two kernels)
+            scored[c] = one_stream ? nullptr : tm.mark(ss);
+        }
+        // (one stream: the chunk's merge starts the status words itself)
+        const bool init_in_merge = one_stream && live_cap;
+        if (live_cap && !init_in_merge) OK(pass_init(sc));
+        // speculative slots: as many as the previous pass of this shape needed
+        // (consecutive passes over similar clusters stop alike), enqueued before
+        // the first status round trip; a slot whose walk is not halted exits at
+        // once.  Not with a communicator: every rank must issue the same slots.
+        // A node-shard pass's chunks merge and exchange on their own stream (sx,
+        // the commit stream's communicator and CUs) and the commit stream only
+        // commits, each commit waiting for its chunk's merged lists: with every
+        // chunk's merge -> all-gather -> merge -> commit chain on the commit
+        // stream the chains of the last two chunks ran back to back after the
+        // scoring (~108 us each at G = 8 with six shard chunks); now one chunk's
+        // exchange overlaps the previous chunk's commit.  The tail chunk merges
+        // and exchanges on its scoring stream right behind its cost launch (its
+        // stream's own communicator and gather buffers, so the collectives of
+        // each communicator stay on one stream in one order) and commits there
+        // after the commit stream's last commit.
+        const bool xs_mode = exchanging(ctx) && !one_stream;
+        // the tail chunk's stream waits for the commit stream's last commit: by
+        // the device word behind each commit (launch_flag_set / flag_wait) once a
+        // commit has run on the commit stream, else by an event (a one-chunk pass
+        // with a communicator: only the pass init is on the commit stream)
+        auto *cflag = ctx->commit_flag.as<uint64_t>();
+        auto after_commits = [&](hipStream_t s) -> int {
+            if (chunks.size() > 1)
+                HIPCK(nas::launch_flag_wait(s, cflag, ctx->commit_seq, halt, commit_wait_ms));
+            else HIPCK(hipStreamWaitEvent(s, tm.mark(sc), 0));
+            return NAS_OK;
+        };
+        hipStream_t sx = nullptr;
+        if (xs_mode) OK(exchange_stream(ctx, &sx));
+        for (size_t c = 0; c < chunks.size(); ++c) {
+            const int lo = chunks[c].first, hi = chunks[c].second;
+            // the last chunk is merged and committed on its own scoring stream
+            // behind the commit stream's earlier work (long finished by then), so
+            // the pass's serial tail after the last cost launch has no
+            // cross-stream hop in front of its merge (the communicator is the
+            // commit stream's: its collectives stay in one order)
+            const bool tail = !one_stream && c + 1 == chunks.size();
+            const bool last = c + 1 == chunks.size();
+            hipStream_t cs = sc;
+            if (xs_mode) {
+                if (tail) {
+                    cs = ss2[c & 1];
+                    OK(merge_range(ctx, tm, lo, hi, cs, (c & 1) ? CH_SCORE2 : CH_SCORE, (int)(c & 1),
+                                   main_view(ctx)));
+                    OK(after_commits(cs));
+                } else {
+                    HIPCK(hipStreamWaitEvent(sx, scored[c], 0));
+                    OK(merge_range(ctx, tm, lo, hi, sx, CH_COMMIT, 2, main_view(ctx)));
+                    HIPCK(hipStreamWaitEvent(sc, tm.mark(sx), 0));
+                }
             } else {
-                HIPCK(hipStreamWaitEvent(sx, scored[c], 0));
-                OK(merge_range(ctx, tm, lo, hi, sx, CH_COMMIT, 2, main_view(ctx)));
-                HIPCK(hipStreamWaitEvent(sc, tm.mark(sx), 0));
+                if (tail) {
+                    cs = ss2[c & 1];
+                    OK(after_commits(cs));
+                } else if (!one_stream) {
+                    HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
+                }
+                // (merging the tail chunk locally before this wait, gated before
+                // its exchange / commit, measured within noise at G = 1 and 8:
+                // profiles/r04_ab_tail.txt)
+                OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx),
+                               init_in_merge ? halt : nullptr));
             }
-        } else {
-            if (tail) {
-                cs = ss2[c & 1];
-                OK(after_commits(cs));
-            } else if (!one_stream) {
-                HIPCK(hipStreamWaitEvent(sc, scored[c], 0));
+            hipEvent_t c0 = tm.fine(cs);
+            // the pass's last commit also writes the status words into the pinned
+            // host area when nothing follows it (no speculative slots): the host
+            // then waits for that commit alone, with no status copy behind it
+            HIPCK(nas::launch_commit(cs, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                                     ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
+                                     ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
+                                     1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr,
+                                     last && status_in_commit ? hs : nullptr));
+            // (releases the tail chunk's commit)
+            if (!one_stream && !last) {
+                if (c + 2 == chunks.size() && ctx->opt_inject_commit_stall_ms > 0) {
+                    (void)nas::launch_stall(cs, ctx->opt_inject_commit_stall_ms);  // (test option)
+                    ctx->opt_inject_commit_stall_ms = 0;
+                }
+                HIPCK(nas::launch_flag_set(cs, cflag, ++ctx->commit_seq));
             }
-            // (merging the tail chunk locally before this wait, gated before
-            // its exchange / commit, measured within noise at G = 1 and 8:
-            // profiles/r04_ab_tail.txt)
-            OK(merge_range(ctx, tm, lo, hi, cs, CH_COMMIT, 0, main_view(ctx),
-                           init_in_merge ? halt : nullptr));
+            tm.span(T_COMMIT, c0, tm.fine(cs));
+            // the commit wrote this chunk's results into the pinned stage as it
+            // ended, and the host unpacks them while later chunks still run.
+            // Stage ordering rule: every stage row the host reads
+            // has ONE writer in the pass -- this commit kernel (to_stage), or
+            // fetch()'s copies on `st` issued after the host has waited for every
+            // landed event -- and the host reads it only after waiting on an
+            // event recorded on the writer's stream behind the writer.  No D2H
+            // copy into the stage runs on a scoring stream (round 4's TAIL_SDMA
+            // variant moved the last chunk's rows to such a copy and returned
+            // stale rows: profiles/r05e_stage_order_probe.txt)
+            landed.push_back({lo, hi, tm.mark(cs)});
         }
-        hipEvent_t c0 = tm.fine(cs);
-        // the pass's last commit also writes the status words into the pinned
-        // host area when nothing follows it (no speculative slots): the host
-        // then waits for that commit alone, with no status copy behind it
-        HIPCK(nas::launch_commit(cs, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
-                                 ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(), N,
-                                 ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(), halt,
-                                 1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr,
-                                 last && status_in_commit ? hs : nullptr));
-        // (releases the tail chunk's commit)
-        if (!one_stream && !last) {
-            if (c + 2 == chunks.size() && ctx->opt_inject_commit_stall_ms > 0) {
-                (void)nas::launch_stall(cs, ctx->opt_inject_commit_stall_ms);  // (test option)
-                ctx->opt_inject_commit_stall_ms = 0;
-            }
-            HIPCK(nas::launch_flag_set(cs, cflag, ++ctx->commit_seq));
-        }
-        tm.span(T_COMMIT, c0, tm.fine(cs));
-        // the commit wrote this chunk's results into the pinned stage as it
-        // ended, and the host unpacks them while later chunks still run.
-        // Stage ordering rule: every stage row the host reads
-        // has ONE writer in the pass -- this commit kernel (to_stage), or
-        // fetch()'s copies on `st` issued after the host has waited for every
-        // landed event -- and the host reads it only after waiting on an
-        // event recorded on the writer's stream behind the writer.  No D2H
-        // copy into the stage runs on a scoring stream (round 4's TAIL_SDMA
-        // variant moved the last chunk's rows to such a copy and returned
-        // stale rows: profiles/r05e_stage_order_probe.txt)
-        landed.push_back({lo, hi, tm.mark(cs)});
+        // st must follow everything: the last chunk's stream followed the commit
+        // stream, which followed every earlier chunk's scoring (and, with xs_mode,
+        // every earlier chunk's exchange); so st waits only when the last chunk
+        // ran on another stream
+        if (!one_stream && ss2[(chunks.size() - 1) & 1] != st)
+            HIPCK(hipStreamWaitEvent(st, tm.mark(ss2[(chunks.size() - 1) & 1]), 0));
+        // (the tail followed the commit stream by the device word, not a stream
+        // wait: st follows the commit stream itself)
+        if (!one_stream && chunks.size() > 1) HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
     }
-    // st must follow everything: the last chunk's stream followed the commit
-    // stream, which followed every earlier chunk's scoring (and, with xs_mode,
-    // every earlier chunk's exchange); so st waits only when the last chunk
-    // ran on another stream
-    if (!one_stream && ss2[(chunks.size() - 1) & 1] != st)
-        HIPCK(hipStreamWaitEvent(st, tm.mark(ss2[(chunks.size() - 1) & 1]), 0));
-    // (the tail followed the commit stream by the device word, not a stream
-    // wait: st follows the commit stream itself)
-    if (!one_stream && chunks.size() > 1) HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
     if (has_coll(ctx)) inject_stall(ctx, st);  // behind every collective of the pass
     for (int r = 0; r < spec; ++r) OK(gathered_slot(ctx, tm, st, CH_SCORE, nullptr, P));
-    if (spec > 0) {
+    if (late_slots) {
         // behind the slots, all placements again: when they finished the walk,
         // the status round trip below brings the final results with it
         HIPCK(hipMemcpyAsync(stage_spec, ctx->out_node.p, (size_t)P * 4, hipMemcpyDeviceToHost,
@@ -2613,7 +2677,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     }
     OK(wait_event(ctx, t1));  // t1 follows the status words (copy, or the last commit)
     int checks = 0;
-    if (spec > 0 && hs[0] < 0 && hs[1] > 0) {
+    if (late_slots && hs[0] < 0 && hs[1] > 0) {
         // speculative slots finished a walk that had halted: the per-chunk
         // copies behind the commits predate them; the full copy behind the
         // slots (same round trip, its own staging area) holds the final
@@ -2649,7 +2713,7 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         if (++checks > P + 1) return nas::fail(ctx, NAS_ERR_HIP, "commit made no progress");
         // (with speculative slots the walk may have resumed and halted again:
         // its first halt is status word 3)
-        if (h0 < 0) h0 = spec > 0 ? (hs[1] > 0 ? std::min(std::max(hs[3], 0), hs[0]) : hs[0]) : hs[0];
+        if (h0 < 0) h0 = late_slots ? (hs[1] > 0 ? std::min(std::max(hs[3], 0), hs[0]) : hs[0]) : hs[0];
         for (int r = 0, n = gather_batch(checks, ctx->cache_active); r < n; ++r)
             OK(gathered_slot(ctx, tm, st, CH_SCORE, nullptr, P));
         OK(fetch());
@@ -2671,6 +2735,10 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
     ctx->timings.commit_rounds = hs[2];
     ctx->slot_hint = std::min(hs[1], MAX_SPEC_SLOTS);
     ctx->last_rescore_rounds = hs[1];
+    if (hs[1] >= HERD_MIN_ROUNDS) {
+        ctx->herd_P = P;
+        ctx->herd_N = N;
+    }
     ctx->slot_hint_P = P;
     ctx->slot_hint_N = N;
     ctx->scored = true;

@@ -220,6 +220,8 @@ struct nas_ctx {
     int32_t opt_synth_profile = 0;          // NAS_OPT_SYNTH_PROFILE
     int32_t opt_commit_cus = 0;             // NAS_OPT_COMMIT_CUS (world 1)
     int32_t opt_cost_cache = 2;             // NAS_OPT_COST_CACHE: 0 off, 1 on, 2 auto
+    int32_t opt_herd_plan = 2;              // NAS_OPT_HERD_PLAN: 0 off, 1 on, 2 auto
+    int32_t herd_P = -1, herd_N = -1;       // auto: the shape whose passes run the herd plan
     bool poisoned = false;       // a collective missed its deadline: communicators aborted
     // timing events, created once and reused by every call (hipEventCreate
     // per mark cost a small placement more than its kernels)

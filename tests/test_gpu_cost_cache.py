@@ -1,4 +1,6 @@
-"""The cost-row cache (NAS_OPT_COST_CACHE, k_rescore_cached): a pass's main
+"""The herd plan (NAS_OPT_HERD_PLAN: chunk after chunk -- fit + cost, merge,
+commit -- on one stream, so every chunk's fit sees its predecessors'
+commits) and the cost-row cache (NAS_OPT_COST_CACHE, k_rescore_cached): a pass's main
 cost launches also store every (pod, node) cost, and its gathered rescore
 slots build a dry pod's new 8-list from the pod's cached row against the
 capacity now instead of re-running fit + contraction + merge.  The lists --
@@ -32,11 +34,12 @@ def _upload(e, WA, L, free, req, dtype="i8"):
 
 
 @pytest.mark.parametrize("P,N,crowd", [(12000, 1500, 40), (20000, 700, 24), (40000, 3000, 0)])
-@pytest.mark.parametrize("mode", [0, 1])
-def test_cache_on_off_equal_oracle(engine, P, N, crowd, mode):
+@pytest.mark.parametrize("mode,herd", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_cache_on_off_equal_oracle(engine, P, N, crowd, mode, herd):
     WA, L, free, req = _herd(P + N + crowd, P, N, crowd)
     want, wcost, wfree = oracle.place(WA, L, req, free, "i8")
     engine.set_option("COST_CACHE", mode)
+    engine.set_option("HERD_PLAN", herd)
     try:
         _upload(engine, WA, L, free, req)
         for _ in range(2):
@@ -45,30 +48,35 @@ def test_cache_on_off_equal_oracle(engine, P, N, crowd, mode):
             bad = np.nonzero(node != want)[0]
             assert len(bad) == 0, (mode, bad[:8], node[bad[:8]], want[bad[:8]])
             assert (score == wcost).all() and (engine.get_capacity() == wfree).all()
-        if crowd:
+        if crowd and not herd:
             assert engine.timings()["rescore_rounds"] > 0
     finally:
         engine.set_option("COST_CACHE", 2)
+        engine.set_option("HERD_PLAN", 2)
 
 
-def test_cache_auto_turns_on_for_a_herd_and_keeps_results(engine):
+def test_auto_herd_plan_and_cache_keep_results():
     """Full-range operands: a global herd.  The first pass
-    rescores without the cache; the second (auto: the first needed >= 4
-    rounds) with it -- identical placements, fewer device-side costs."""
-    engine.synth_cluster(0x4E4153, 3000, 40000, "i8", peers=8, profile=1)
-    engine.set_option("COST_CACHE", 2)
-    engine.reset_capacity()
-    n1, _, s1 = engine.place()
-    t1 = engine.timings()
-    assert t1["rescore_rounds"] >= 4, t1
-    engine.reset_capacity()
-    n2, _, s2 = engine.place()
-    t2 = engine.timings()
-    assert (n1 == n2).all() and (s1 == s2).all()
-    WA, L, cap, req = engine.read_inputs(0, 40000, want_L=True)
-    want, wcost, _ = oracle.place(WA, L, req, cap, "i8")
-    assert (n2 == want).all() and (s2 == wcost).all()
-    assert t2["cost_launches"] == t1["cost_launches"]
+    (pipelined plan, no cache) rescores in many rounds; from the second on
+    (auto: its shape needed >= 8 rounds) the herd plan and the cache --
+    identical placements, far fewer rescore rounds."""
+    with Engine(0) as e:
+        e.synth_cluster(0x4E4153, 3000, 60000, "i8", peers=8, profile=1)
+        e.reset_capacity()
+        n1, _, s1 = e.place()
+        t1 = e.timings()
+        assert t1["rescore_rounds"] >= 8, t1
+        res = []
+        for _ in range(2):
+            e.reset_capacity()
+            n2, _, s2 = e.place()
+            res.append(e.timings())
+            assert (n1 == n2).all() and (s1 == s2).all()
+        WA, L, cap, req = e.read_inputs(0, 60000, want_L=True)
+        want, wcost, _ = oracle.place(WA, L, req, cap, "i8")
+        assert (n1 == want).all() and (s1 == wcost).all()
+        # (the herd plan's chunks differ from the pipelined plan's)
+        assert res[-1]["cost_launches"] != t1["cost_launches"], (t1, res)
 
 
 def test_cache_bf16_herd_equals_oracle(engine):

@@ -13,8 +13,18 @@ import sys
 rows = []
 for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
     rows += list(csv.DictReader(open(f)))
+for f in glob.glob(sys.argv[1] + "/**/*.db", recursive=True):  # rocprofv3's default (rocpd) output
+    import sqlite3
+    con = sqlite3.connect(f)
+    rows += [{"Start_Timestamp": a, "End_Timestamp": b, "Kernel_Name": n, "Queue_Id": q, "Grid_Size_X": g}
+             for a, b, n, q, g in con.execute("select start, end, name, queue_id, grid_x from kernels")]
+def kname(n):
+    m = re.search(r"(k_[a-z0-9_]+|__amd_[a-zA-Z_]+|ncclDevKernel[a-zA-Z_0-9]*|Cijk_[A-Za-z0-9]+)", n)
+    return m.group(1) if m else n[:24]
+
+
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
-             re.search(r"(k_[a-z0-9_]+|__amd_[a-zA-Z_]+|ncclDevKernel[a-zA-Z_0-9]*)", r["Kernel_Name"]).group(1),
+             kname(r["Kernel_Name"]),
              r["Queue_Id"], r["Grid_Size_X"]) for r in rows)
 
 
