@@ -59,6 +59,21 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
         }
         return;
     }
+    // blocks wholly below the first pod take no part (no words, no ticket):
+    // the launch covers [p0, P) but the halt is usually far into it (the
+    // herd plan's slots scan from the pass's start behind every chunk; with
+    // every block fencing and drawing a ticket a scan cost ~90 us on the few
+    // CUs beside a cost launch)
+    const int b_first = (first - p0) / STALE_THREADS;
+    if (b_first >= (int)gridDim.x) {  // (a halt word past the scan: nothing to flag)
+        if (blockIdx.x == 0 && tid == 0) {
+            ctl[0] = -1;
+            ctl[1] = 0;
+        }
+        return;
+    }
+    if ((int)blockIdx.x < b_first) return;
+    const int participants = (int)gridDim.x - b_first;
     bool dry = false;
     if (p < P && p >= first) {
         const u64 b = bound[p];
@@ -86,7 +101,7 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int ticket = __hip_atomic_fetch_add(ctl + 3, 1, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
-        last = ticket == (int)gridDim.x - 1;
+        last = ticket == participants - 1;
         if (last) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -94,9 +109,10 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
     }
     __syncthreads();
     if (!last) return;
-    // ---- compaction by the last block
-    const int per = (n_words + STALE_THREADS - 1) / STALE_THREADS;
-    const int w0 = min(n_words, tid * per), w1 = min(n_words, w0 + per);
+    // ---- compaction by the last block (words of the participating blocks)
+    const int wbase = b_first * (STALE_THREADS / 64), nw = n_words - wbase;
+    const int per = (nw + STALE_THREADS - 1) / STALE_THREADS;
+    const int w0 = wbase + min(nw, tid * per), w1 = min(n_words, w0 + per);
     int c = 0;
     for (int w = w0; w < w1; ++w) c += __popcll(words[w]);
     part[tid] = c;

@@ -101,7 +101,7 @@ constexpr size_t CACHE_MAX_BYTES = (size_t)16 << 30;
 // NAS_OPT_HERD_PLAN auto: rescore rounds of one pass that make its shape a herd
 constexpr int HERD_MIN_ROUNDS = 8;
 // gathered slots behind each chunk's commit in the herd plan
-constexpr int HERD_SLOTS = 3;
+constexpr int HERD_SLOTS = 1;
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
 constexpr int MAX_SPEC_SLOTS = 8;         // speculative slots at most (nas_place, slot_hint)
 // ... except the second check: a walk still halted after a full batch is
@@ -1195,14 +1195,19 @@ std::vector<std::pair<int, int>> plan_chunks(const nas_ctx *ctx, bool herd = fal
     const int P = ctx->P;
     const bool wide = tile_pods(ctx) != nas::COST_BN && ctx->world == 1;
     if (herd) {
-        // the herd plan's chunks, one after another on one stream: ~1.25 pods
-        // per node each (a chunk's own pods compete for the nodes its fit saw
-        // free; tools/herd_model.py), at most 48 units (C3: 32 wide tiles =
-        // 1,280 workgroups over 40 node tiles, whole waves), whole cost tiles
-        const int unit = tile_pods(ctx) / std::gcd(tile_pods(ctx), nas::COST_BN);
-        int units = (int)std::min<int64_t>(CHUNK_TILES_WIDE, (5LL * ctx->N / 4 + nas::COST_BN - 1) / nas::COST_BN);
-        units = std::max(unit, (units + unit - 1) / unit * unit);
-        const int step = units * nas::COST_BN;
+        // the herd plan's chunks (nas_place): ONE wave of cost workgroups
+        // each -- as many pod tiles as the CUs hold beside this rank's node
+        // tiles (C3: 6 wide tiles = 2,304 pods over 40 node tiles = 240
+        // workgroups), so the commit stream keeps the CUs left over -- and at
+        // most ~1.25 pods per node (a chunk's own pods compete for the nodes
+        // its fit saw free; tools/herd_model.py: 0 slots at 3,072 pods per
+        // chunk, 5 at 6,144, 18 at 12,288 for 36,864 pods over 10k nodes)
+        const int tp = tile_pods(ctx);
+        int tiles = std::min(ctx->n_cu / std::max(plan_n_mt(ctx), 1),
+                             std::max(1, (int)((5LL * ctx->N / 4) / tp)));
+        if (tp != nas::COST_BN) tiles = std::max(2, tiles / 2 * 2);  // whole 256-pod units
+        tiles = std::max(tiles, 1);
+        const int step = tiles * tp;
         for (int lo = 0; lo < P; lo += step) chunks.push_back({lo, std::min(P, lo + step)});
         return chunks;
     }
@@ -2388,19 +2393,20 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         ~CacheOff() { c->cache_active = false; }
     } cache_off{ctx};
     ctx->cache_active = false;
+    // (the herd plan below, auto: sticky for a shape once one of its passes
+    // needed HERD_MIN_ROUNDS rescore rounds; it turns the cache on too)
+    const bool herd_shape = !has_coll(ctx) &&
+                            (ctx->opt_herd_plan == 1 ||
+                             (ctx->opt_herd_plan == 2 && ctx->herd_P == P && ctx->herd_N == N));
     if (ctx->opt_cost_cache != 0) {
         const bool herd = ctx->slot_hint_P == P && ctx->slot_hint_N == N &&
                           ctx->last_rescore_rounds >= CACHE_MIN_ROUNDS;
         const size_t bytes = (size_t)ctx->Pp * ctx->Mp * 4;
-        if ((ctx->opt_cost_cache == 1 || herd) && bytes <= CACHE_MAX_BYTES)
+        if ((ctx->opt_cost_cache == 1 || herd || herd_shape) && bytes <= CACHE_MAX_BYTES)
             ctx->cache_active = nas::ensure(ctx, ctx->cost_cache, bytes) == NAS_OK;
         if (!ctx->cache_active) ctx->err.clear();  // (no memory: the slots recompute)
     }
-    // the herd plan (NAS_OPT_HERD_PLAN; below): auto = sticky for a shape
-    // once one of its passes needed HERD_MIN_ROUNDS rescore rounds
-    const bool herd = !has_coll(ctx) &&
-                      (ctx->opt_herd_plan == 1 ||
-                       (ctx->opt_herd_plan == 2 && ctx->herd_P == P && ctx->herd_N == N));
+    const bool herd = herd_shape;
     hipEvent_t t0 = tm.mark(st);
     // Each chunk is filtered against the working capacity as the commit
     // stream has left it so far: every value read is >= the capacity at the
@@ -2472,37 +2478,45 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
         : has_coll(ctx)             ? (ctx->opt_comm_timeout_ms > 0 ? ctx->opt_comm_timeout_ms : 600000)
                                     : 2000;
     if (herd) {
-        // The herd plan: chunk after chunk on one stream -- fit + cost, merge,
-        // commit -- so every chunk's fused fit reads the capacity its
-        // predecessors' commits left (lag 1) instead of a capacity two or
-        // more chunks stale.  In a global herd (configs.C3_fullrange: every
-        // pod ranks the same nodes first) the pipelined plan's stale lists
-        // run dry for most pods and the walk rescored ~90% of them in ~90
-        // gathered slots; a CPU model of the walk (tools/herd_model.py,
-        // profiles/r06e_herd_model.txt) needs 15 slots at lag 2, 1 at lag 1.  The
-        // cost is the scoring / commit overlap: each chunk's merge and commit
-        // run with the GPU otherwise idle.
+        // The herd plan: chunks of one wave of cost workgroups, scored and
+        // merged back to back on one stream; each chunk's commit and
+        // HERD_SLOTS gathered slots run on the commit stream, on the CUs that
+        // wave leaves free, while the next chunk's workgroups run their main loop
+        // -- so the next chunk's fused fit, read after that loop, sees this
+        // chunk's commits (lag ~1) instead of a capacity two or more chunks
+        // stale.  In a global herd (configs.C3_fullrange: every pod ranks the
+        // same nodes first) the pipelined plan's stale lists run dry for most
+        // pods: ~90 gathered slots per C3 pass.  The slots here rescore from
+        // the cost-row cache only (their recomputing form would share the
+        // scoring buffers with the next chunk's launch); without it a halt
+        // waits for the host loop.
         if (live_cap) OK(pass_init(st));
+        HIPCK(hipStreamWaitEvent(sc, tm.mark(st), 0));
         for (size_t c = 0; c < chunks.size(); ++c) {
             const int lo = chunks[c].first, hi = chunks[c].second;
             const bool last = c + 1 == chunks.size();
+            // (the merge on the scoring stream, behind its cost launch, with
+            // the whole GPU: ~10 us; on the commit stream's leftover CUs it
+            // took ~60 us, and the commit stream fell behind the scoring)
             OK(score_range(ctx, tm, lo, hi, st, score_cap, nullptr, false));
             OK(merge_range(ctx, tm, lo, hi, st, CH_SCORE, 0, main_view(ctx)));
-            hipEvent_t c0 = tm.fine(st);
-            HIPCK(nas::launch_commit(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+            HIPCK(hipStreamWaitEvent(sc, tm.mark(st), 0));
+            hipEvent_t c0 = tm.fine(sc);
+            HIPCK(nas::launch_commit(sc, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
                                      ctx->req.as<int32_t>(), ctx->Pp, lo, hi, ctx->cap.as<int32_t>(),
                                      N, ctx->out_node.as<int32_t>(), ctx->out_cost_i.as<int32_t>(),
                                      halt, 1, pub, zrow_ptr(ctx), stage, want_raw ? stage + P : nullptr,
                                      last && status_in_commit ? hs : nullptr));
-            tm.span(T_COMMIT, c0, tm.fine(st));
-            // a walk halted in this chunk resumes here, before the next chunk
-            // is scored against the capacity it leaves: HERD_SLOTS gathered
-            // slots over the pods scored so far (hi), each a few idle launches
-            // when nothing halted; a halt they leave is resumed by the next
-            // chunk's slots or the host loop below
-            for (int r = 0; r < HERD_SLOTS; ++r) OK(gathered_slot(ctx, tm, st, CH_SCORE, pub, hi));
-            landed.push_back({lo, hi, tm.mark(st)});
+            tm.span(T_COMMIT, c0, tm.fine(sc));
+            // a walk halted in this chunk resumes here, before the chunk after
+            // next is scored (a halt they leave is resumed by a later chunk's
+            // slots or the host loop below); idle slots are three launches
+            // that exit at once
+            if (ctx->cache_active)
+                for (int r = 0; r < HERD_SLOTS; ++r) OK(gathered_slot(ctx, tm, sc, CH_SCORE, pub, hi));
+            landed.push_back({lo, hi, tm.mark(sc)});
         }
+        HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
     } else {
         const hipStream_t ss2[2] = {st, ctx->stream2};
         if (!one_stream) {
