@@ -39,6 +39,27 @@ constexpr int STALE_MIN_FIT = 2;
 // words are stored, drained (vmcnt(0)), released at agent scope by thread 0,
 // then the ticket is drawn; the last block acquires before reading
 // (cdna_hip_programming.md, the split-K counter recipe).
+// pod p's list is dry: incomplete (bound != KEY_INVALID) and fewer than
+// STALE_MIN_FIT of its usable candidates fit the capacity now
+__device__ __forceinline__ bool stale_pod(const u64 *__restrict__ key, const u64 *__restrict__ bound,
+                                          const int *__restrict__ req, int Pp,
+                                          const int *__restrict__ cap, int N, int p) {
+    const u64 b = bound[p];
+    if (b == KEY_INVALID) return false;
+    u64 k[KC];
+    load8(key + (size_t)p * KC, k);
+    const int r0 = req[p], r1 = req[Pp + p], r2 = req[2 * Pp + p];
+    int fits = 0;
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+        if (k[j] == KEY_INVALID || k[j] > b) break;
+        const int n = (int)(unsigned)k[j];
+        fits += (r0 <= cap[n] && r1 <= cap[N + n] && r2 <= cap[2 * N + n]) ? 1 : 0;
+        if (fits >= STALE_MIN_FIT) break;
+    }
+    return fits < STALE_MIN_FIT;
+}
+
 __global__ void __launch_bounds__(STALE_THREADS)
 k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *__restrict__ req,
         int Pp, const int *__restrict__ cap, int N, int p0, int P, u64 *__restrict__ words,
@@ -47,68 +68,44 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
     __shared__ int part[STALE_THREADS];
     __shared__ int last;
     const int tid = threadIdx.x;
-    const int t = blockIdx.x * STALE_THREADS + tid;
-    const int p = p0 + t;
     // device-side slot: pods from the halt word on; nothing halted -> an
     // empty view, published by block 0 alone
     const int first = p0_dev ? *p0_dev : p0;
-    if (first < 0) {
-        if (blockIdx.x == 0 && tid == 0) {
-            ctl[0] = -1;
-            ctl[1] = 0;
-        }
-        return;
-    }
     // blocks wholly below the first pod take no part (no words, no ticket):
     // the launch covers [p0, P) but the halt is usually far into it (the
-    // herd plan's slots scan from the pass's start behind every chunk; with
-    // every block fencing and drawing a ticket a scan cost ~90 us on the few
-    // CUs beside a cost launch)
-    const int b_first = (first - p0) / STALE_THREADS;
-    if (b_first >= (int)gridDim.x) {  // (a halt word past the scan: nothing to flag)
+    // herd plan's slots scan from the pass's start behind every chunk)
+    const int b_first = first < 0 ? 0 : (first - p0) / STALE_THREADS;
+    if (first < 0 || b_first >= (int)gridDim.x) {  // (or a halt word past the scan)
         if (blockIdx.x == 0 && tid == 0) {
             ctl[0] = -1;
             ctl[1] = 0;
         }
         return;
     }
-    if ((int)blockIdx.x < b_first) return;
-    const int participants = (int)gridDim.x - b_first;
-    bool dry = false;
-    if (p < P && p >= first) {
-        const u64 b = bound[p];
-        if (b != KEY_INVALID) {
-            u64 k[KC];
-            load8(key + (size_t)p * KC, k);
-            const int r0 = req[p], r1 = req[Pp + p], r2 = req[2 * Pp + p];
-            int fits = 0;
-#pragma unroll
-            for (int j = 0; j < KC; ++j) {
-                if (k[j] == KEY_INVALID || k[j] > b) break;
-                const int n = (int)(unsigned)k[j];
-                fits += (r0 <= cap[n] && r1 <= cap[N + n] && r2 <= cap[2 * N + n]) ? 1 : 0;
-                if (fits >= STALE_MIN_FIT) break;
-            }
-            dry = fits < STALE_MIN_FIT;
-        }
-    }
-    const u64 m = __ballot(dry);
-    if ((tid & 63) == 0) words[t >> 6] = m;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    {
+        const int t = blockIdx.x * STALE_THREADS + tid;
+        const int p = p0 + t;
+        if ((int)blockIdx.x < b_first) return;
+        const int participants = (int)gridDim.x - b_first;
+        const bool dry = p < P && p >= first && stale_pod(key, bound, req, Pp, cap, N, p);
+        const u64 m = __ballot(dry);
+        if ((tid & 63) == 0) words[t >> 6] = m;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int ticket = __hip_atomic_fetch_add(ctl + 3, 1, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        last = ticket == participants - 1;
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int ticket = __hip_atomic_fetch_add(ctl + 3, 1, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            last = ticket == participants - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
         }
+        __syncthreads();
+        if (!last) return;
     }
-    __syncthreads();
-    if (!last) return;
     // ---- compaction by the last block (words of the participating blocks)
     const int wbase = b_first * (STALE_THREADS / 64), nw = n_words - wbase;
     const int per = (nw + STALE_THREADS - 1) / STALE_THREADS;

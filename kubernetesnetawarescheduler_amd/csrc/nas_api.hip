@@ -102,6 +102,10 @@ constexpr size_t CACHE_MAX_BYTES = (size_t)16 << 30;
 constexpr int HERD_MIN_ROUNDS = 8;
 // gathered slots behind each chunk's commit in the herd plan
 constexpr int HERD_SLOTS = 1;
+// ... of at most this many pods (they run on the CUs a chunk's wave leaves
+// free, C3: 16, where a 2,048-pod rescore takes ~190 us; 512-pod slots
+// measured no faster and less stable: profiles/r06e_ab_herd.txt)
+constexpr int HERD_SLOT_PODS = 2048;
 constexpr int GATHER_SLOTS_PER_SYNC = 4;  // gathered slots enqueued per host check of the halt word
 constexpr int MAX_SPEC_SLOTS = 8;         // speculative slots at most (nas_place, slot_hint)
 // ... except the second check: a walk still halted after a full batch is
@@ -767,8 +771,10 @@ int score_range(nas_ctx *ctx, Timer &tm, int p_lo, int p_hi, hipStream_t st = nu
 // kernel exits at once (the exchange still runs, so all ranks issue the same
 // collectives).  Slots need no host round trip, so a crowded cluster's many
 // stops cost launches, not synchronisations.
-int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, int ch, int32_t *pub, int hi) {
-    const int R = std::min(ctx->cache_active ? GATHER_PODS_CACHED : GATHER_PODS, ctx->Pp);
+int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, int ch, int32_t *pub, int hi,
+                  int r_max = 0) {
+    const int R = std::min({ctx->cache_active ? GATHER_PODS_CACHED : GATHER_PODS, ctx->Pp,
+                            r_max > 0 ? r_max : ctx->Pp});
     OK(nas::ensure(ctx, ctx->g_words, (size_t)nas::stale_words(ctx->Pp) * 8));
     OK(nas::ensure(ctx, ctx->g_idx, (size_t)R * 4));
     OK(nas::ensure(ctx, ctx->g_key, (size_t)R * KC * 8));
@@ -2513,7 +2519,8 @@ int nas_place(nas_ctx *ctx, int32_t *node_out, float *cost_out, int64_t *int_sco
             // slots or the host loop below); idle slots are three launches
             // that exit at once
             if (ctx->cache_active)
-                for (int r = 0; r < HERD_SLOTS; ++r) OK(gathered_slot(ctx, tm, sc, CH_SCORE, pub, hi));
+                for (int r = 0; r < HERD_SLOTS; ++r)
+                    OK(gathered_slot(ctx, tm, sc, CH_SCORE, pub, hi, HERD_SLOT_PODS));
             landed.push_back({lo, hi, tm.mark(sc)});
         }
         HIPCK(hipStreamWaitEvent(st, tm.mark(sc), 0));
