@@ -221,6 +221,16 @@ def launch_ranks(child_argv, n, ndev, timeout_s=None, extra_env=None):
     tmp = tempfile.mkdtemp(prefix="nas_ranks_", dir="/tmp")
     out0 = os.path.join(tmp, "rank0.out")
     procs, failed = [], None
+
+    def die_with_parent():
+        # a rank must not outlive this launcher (a driver that kills it on a
+        # deadline would otherwise leave the ranks on the GPUs): SIGKILL on
+        # the parent's death (Linux PR_SET_PDEATHSIG)
+        try:
+            import ctypes
+            ctypes.CDLL(None).prctl(1, 9)
+        except Exception:  # noqa: BLE001 -- best effort off Linux
+            pass
     try:
         with open(out0, "w") as f0:
             for r in range(n):
@@ -228,7 +238,7 @@ def launch_ranks(child_argv, n, ndev, timeout_s=None, extra_env=None):
                            WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
                            NAS_DIST_INIT="file://" + os.path.join(tmp, "rdv"),
                            MASTER_ADDR="127.0.0.1", **(extra_env or {}))
-                procs.append(subprocess.Popen(child_argv, env=env,
+                procs.append(subprocess.Popen(child_argv, env=env, preexec_fn=die_with_parent,
                                               stdout=f0 if r == 0 else subprocess.DEVNULL))
             deadline = None if timeout_s is None else time.monotonic() + timeout_s
             rcs = [None] * n

@@ -94,3 +94,43 @@ def test_main_self_launches_without_world_size(monkeypatch, capsys):
     assert seen["n"] == 2 and seen["argv"][-4:] == ["--gpus", "2", "--steps", "1"]
     out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert out["n_gpus"] == 2 and "self-launch" in out["config"]["launcher"]
+
+
+def test_ranks_die_with_the_launcher(tmp_path):
+    """A driver that kills the launcher on a deadline must not leave its rank
+    processes running (PR_SET_PDEATHSIG)."""
+    import signal
+    import subprocess
+    pids = tmp_path / "pids"
+    child = ("import os, time\n"
+             f"open({str(pids)!r} + '.' + os.environ['RANK'], 'w').write(str(os.getpid()))\n"
+             "time.sleep(120)\n")
+    launcher = ("import sys\n"
+                f"sys.path.insert(0, {ROOT!r})\n"
+                "import bench\n"
+                f"bench.launch_ranks([sys.executable, '-c', {child!r}], 2, 1)\n")
+    p = subprocess.Popen([sys.executable, "-c", launcher])
+    files = [tmp_path / f"pids.{r}" for r in range(2)]
+    t0 = time.monotonic()
+    while not all(f.exists() and f.read_text() for f in files):
+        assert time.monotonic() - t0 < 60, "ranks did not start"
+        time.sleep(0.05)
+    ranks = [int(f.read_text()) for f in files]
+    p.send_signal(signal.SIGKILL)
+    p.wait()
+    t0 = time.monotonic()
+    alive = ranks
+    while alive and time.monotonic() - t0 < 20:
+        alive = []
+        for pid in ranks:
+            try:
+                os.kill(pid, 0)
+                with open(f"/proc/{pid}/stat") as f:
+                    if f.read().split()[2] != "Z":
+                        alive.append(pid)
+            except (ProcessLookupError, FileNotFoundError):
+                pass
+        time.sleep(0.1)
+    for pid in alive:  # (never leave them behind, even when the test fails)
+        os.kill(pid, signal.SIGKILL)
+    assert not alive
