@@ -12,6 +12,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <memory>
+#include <cstdlib>
 #include <mutex>
 #include <new>
 #include <numeric>
@@ -1451,8 +1452,8 @@ void reap_comm_helpers(nas_ctx *ctx, int detach_ms = -1) {
 // set of masked queues -- as many as its most concurrent contexts used -- and
 // the runtime's create / destroy path for them runs once per (device, mask)
 // slot, not once per context (tools/stream_churn_probe.hip measures what
-// churning them costs).  The pool is never torn down: its streams live until
-// the process exits, like the runtime's own queue pool.
+// churning them costs).  Idle pooled streams live until the process exits
+// (drain_masked_pool).
 struct MaskedPool {
     struct Slot {
         int dev;
@@ -1466,6 +1467,20 @@ struct MaskedPool {
 MaskedPool &masked_pool() {
     static MaskedPool *p = new MaskedPool;  // (intentionally leaked: outlives static teardown)
     return *p;
+}
+// at exit the idle pooled streams are destroyed while the runtime is still up
+// (the handler is registered after the runtime initialised, so it runs before
+// the runtime's own teardown): left to that teardown, a process under
+// rocprofv3 with masked queues alive crashed in __cxa_finalize after the
+// profiler had finalised (the G = 8 rehearsal trace, gpurun_out/r06k)
+void drain_masked_pool() {
+    MaskedPool &mp = masked_pool();
+    std::lock_guard<std::mutex> g(mp.mu);
+    for (const MaskedPool::Slot &sl : mp.idle) {
+        (void)hipSetDevice(sl.dev);
+        (void)hipStreamDestroy(sl.s);
+    }
+    mp.idle.clear();
 }
 std::atomic<int64_t> g_live_contexts{0};
 
@@ -1483,6 +1498,8 @@ hipError_t masked_acquire(int dev, const std::vector<uint32_t> &mask, hipStream_
     }
     const hipError_t e = hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data());
     if (e != hipSuccess) return e;
+    static std::once_flag at_exit;
+    std::call_once(at_exit, [] { std::atexit(drain_masked_pool); });
     std::lock_guard<std::mutex> g(masked_pool().mu);
     ++mp.created;
     ++mp.lent;
