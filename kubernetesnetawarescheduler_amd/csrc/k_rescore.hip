@@ -138,6 +138,56 @@ k_stale(const u64 *__restrict__ key, const u64 *__restrict__ bound, const int *_
     }
 }
 
+// The herd plan's in-loop slots (nas_place): one workgroup scans the W pods
+// from the halt word on and compacts the flagged ones itself -- no per-block
+// agent-scope release and ticket.  Beside a wave of cost workgroups that
+// store their cost rows (dirty L2 lines), k_stale's per-block release fences
+// (an L2 write-back each) ran 125-165 us per slot against 11 us on an idle
+// GPU (profiles/r06e_herd_timeline.txt); in a herd nearly every pod after the
+// halt is flagged, so W = 2R pods fill the view.
+constexpr int SW_THREADS = 1024;
+__global__ void __launch_bounds__(SW_THREADS)
+k_stale_window(const u64 *__restrict__ key, const u64 *__restrict__ bound,
+               const int *__restrict__ req, int Pp, const int *__restrict__ cap, int N, int P,
+               int W, int R, int *__restrict__ idx, int *__restrict__ ctl,
+               const int *__restrict__ p0_dev) {
+    __shared__ int wc[SW_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int first = *p0_dev;
+    if (first < 0 || first >= P) {  // nothing halted (or past the scan): an empty view
+        if (tid == 0) {
+            ctl[0] = -1;
+            ctl[1] = 0;
+        }
+        return;
+    }
+    const int end = min(P, first + W);
+    int off = 0;  // flagged pods so far (block-uniform)
+    for (int b = first; b < end && off < R; b += SW_THREADS) {
+        const int p = b + tid;
+        const bool dry = p < end && stale_pod(key, bound, req, Pp, cap, N, p);
+        const u64 m = __ballot(dry);
+        if (lane == 0) wc[w] = __popcll(m);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int v = 0; v < SW_THREADS / 64; ++v) {
+            before += v < w ? wc[v] : 0;
+            total += wc[v];
+        }
+        const int pos = off + before + __popcll(m & ((1ull << lane) - 1));
+        if (dry && pos < R) idx[pos] = p;
+        off += total;
+        __syncthreads();  // (wc is rewritten next round)
+    }
+    if (tid == 0) {
+        const int n = min(off, R);
+        ctl[0] = n > 0 ? 0 : -1;
+        ctl[1] = n;
+        ctl[2] += n;
+    }
+}
+
 // Cost-row cache rescoring (round 6).  In a global herd -- every pod ranks
 // the same nodes first (configs.C3_fullrange: uniform random latency, so a
 // node's column sum dominates every pod's cost) -- most pods' lists, scored
@@ -262,6 +312,17 @@ hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t
                                               reinterpret_cast<const u64 *>(bound), req, Pp, cap, N,
                                               p0, P, w, blocks * (STALE_THREADS / 64), R, idx, ctl,
                                               p0_dev);
+    return hipGetLastError();
+}
+
+
+hipError_t launch_stale_window(hipStream_t st, const uint64_t *key, const uint64_t *bound,
+                               const int32_t *req, int Pp, const int32_t *cap, int N, int P, int W,
+                               int R, int32_t *idx, int32_t *ctl, const int32_t *p0_dev) {
+    if (!p0_dev || W <= 0 || R <= 0) return hipErrorInvalidValue;
+    k_stale_window<<<1, SW_THREADS, 0, st>>>(reinterpret_cast<const u64 *>(key),
+                                            reinterpret_cast<const u64 *>(bound), req, Pp, cap, N,
+                                            P, W, R, idx, ctl, p0_dev);
     return hipGetLastError();
 }
 

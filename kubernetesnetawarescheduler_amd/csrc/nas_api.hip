@@ -786,9 +786,16 @@ int gathered_slot(nas_ctx *ctx, Timer &tm, hipStream_t st, int ch, int32_t *pub,
     auto *gk = ctx->g_key.as<uint64_t>();
     auto *gb = ctx->g_bound.as<uint64_t>();
     hipEvent_t e0 = tm.fine(st);
-    HIPCK(nas::launch_stale_scan(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
-                                 ctx->req.as<int32_t>(), ctx->Pp, ctx->cap.as<int32_t>(), ctx->N,
-                                 -1, hi, ctx->g_words.as<uint64_t>(), R, idx, ctl, halt));
+    // (a bounded slot -- the herd plan's, beside a cost wave -- scans a window
+    // of 2R pods from the halt in one workgroup: no release fences)
+    if (r_max > 0)
+        HIPCK(nas::launch_stale_window(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                                       ctx->req.as<int32_t>(), ctx->Pp, ctx->cap.as<int32_t>(),
+                                       ctx->N, hi, 2 * R, R, idx, ctl, halt));
+    else
+        HIPCK(nas::launch_stale_scan(st, ctx->cand_key.as<uint64_t>(), ctx->cand_bound.as<uint64_t>(),
+                                     ctx->req.as<int32_t>(), ctx->Pp, ctx->cap.as<int32_t>(), ctx->N,
+                                     -1, hi, ctx->g_words.as<uint64_t>(), R, idx, ctl, halt));
     const bool xch = exchanging(ctx);
     auto *ck = ctx->cand_key.as<uint64_t>();
     auto *cbnd = ctx->cand_bound.as<uint64_t>();

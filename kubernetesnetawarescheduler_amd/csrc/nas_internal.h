@@ -331,6 +331,11 @@ hipError_t launch_stale_scan(hipStream_t st, const uint64_t *key, const uint64_t
                              const int32_t *req, int Pp, const int32_t *cap, int N, int p0, int P,
                              uint64_t *words, int R, int32_t *idx, int32_t *ctl,
                              const int32_t *p0_dev = nullptr);
+// one workgroup: the flagged pods among [*p0_dev, min(P, *p0_dev + W)), the
+// first R of them, same ctl protocol (the herd plan's in-loop slots)
+hipError_t launch_stale_window(hipStream_t st, const uint64_t *key, const uint64_t *bound,
+                               const int32_t *req, int Pp, const int32_t *cap, int N, int P, int W,
+                               int R, int32_t *idx, int32_t *ctl, const int32_t *p0_dev);
 
 // rescore from the cost-row cache (cache[Pp][stride], this rank's nloc local
 // nodes from global node n0): view row q < ctl[1] (nothing if ctl[0] < 0) is
