@@ -395,6 +395,19 @@ __global__ void k_pass_init(int *__restrict__ status, const int *__restrict__ ca
         for (int i = t; i < n; i += gridDim.x * blockDim.x) cap_snap[i] = cap[i];
 }
 
+// device-to-device copy of n int32 (nas_reset_capacity): a kernel launch
+// costs the host ~5 us where hipMemcpyAsync's device-to-device path cost
+// 15-36 us per call (the marker trace of a reset-then-place cycle,
+// gpurun_out/r06r/prof/trace_place); 16-byte moves, both buffers from hipMalloc
+__global__ void k_copy_i32(int *__restrict__ dst, const int *__restrict__ src, long long n) {
+    const long long n4 = n >> 2;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride)
+        reinterpret_cast<int4 *>(dst)[i] = reinterpret_cast<const int4 *>(src)[i];
+    for (long long i = 4 * n4 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
+        dst[i] = src[i];
+}
+
 __global__ void k_rehearse_replicate(unsigned long long *__restrict__ a, long long n, int G, int N) {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
          i += (long long)gridDim.x * blockDim.x) {
@@ -502,6 +515,14 @@ hipError_t launch_flag_wait(hipStream_t st, const uint64_t *flag, uint64_t v, in
 hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
                             int n) {
     k_pass_init<<<cap_snap ? grid_for(n, 256) : 1, 256, 0, st>>>(status, cap, cap_snap, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_copy_i32(hipStream_t st, int32_t *dst, const int32_t *src, int64_t n) {
+    if (n <= 0) return hipSuccess;
+    if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15)
+        return hipErrorInvalidValue;
+    k_copy_i32<<<grid_for((n + 3) / 4, 256), 256, 0, st>>>(dst, src, (long long)n);
     return hipGetLastError();
 }
 

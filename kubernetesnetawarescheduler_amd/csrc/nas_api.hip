@@ -2031,8 +2031,10 @@ int nas_reset_capacity(nas_ctx *ctx) {
     // streams start behind `ready`), and every host read of the capacity syncs
     // ctx->stream -- the round trip here cost each reset-then-place cycle a
     // launch + wait (~30-50 us; C2's whole pass is ~450 us)
-    HIPCK(hipMemcpyAsync(ctx->cap.p, ctx->cap0.p, (size_t)ctx->B * 3 * ctx->cap_n * 4,
-                         hipMemcpyDeviceToDevice, ctx->stream));
+    // (a copy kernel: hipMemcpyAsync's device-to-device path cost the host
+    // 15-36 us per reset, k_misc.hip k_copy_i32)
+    HIPCK(nas::launch_copy_i32(ctx->stream, ctx->cap.as<int32_t>(), ctx->cap0.as<int32_t>(),
+                               (int64_t)ctx->B * 3 * ctx->cap_n));
     return NAS_OK;
 }
 
