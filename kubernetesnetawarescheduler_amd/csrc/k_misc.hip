@@ -398,9 +398,10 @@ __global__ void k_pass_init(int *__restrict__ status, const int *__restrict__ ca
 // device-to-device copy of n int32 (nas_reset_capacity): a kernel launch
 // costs the host ~5 us where hipMemcpyAsync's device-to-device path cost
 // 15-36 us per call (the marker trace of a reset-then-place cycle,
-// gpurun_out/r06r/prof/trace_place); 16-byte moves, both buffers from hipMalloc
-__global__ void k_copy_i32(int *__restrict__ dst, const int *__restrict__ src, long long n) {
-    const long long n4 = n >> 2;
+// gpurun_out/r06r/prof/trace_place)
+__global__ void k_copy_i32(int *__restrict__ dst, const int *__restrict__ src, long long n,
+                           int vec) {
+    const long long n4 = vec ? n >> 2 : 0;
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride)
         reinterpret_cast<int4 *>(dst)[i] = reinterpret_cast<const int4 *>(src)[i];
@@ -520,9 +521,9 @@ hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap,
 
 hipError_t launch_copy_i32(hipStream_t st, int32_t *dst, const int32_t *src, int64_t n) {
     if (n <= 0) return hipSuccess;
-    if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15)
-        return hipErrorInvalidValue;
-    k_copy_i32<<<grid_for((n + 3) / 4, 256), 256, 0, st>>>(dst, src, (long long)n);
+    // 16-byte moves when both buffers are 16-byte aligned (hipMalloc's), else dwords
+    const bool vec = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) == 0;
+    k_copy_i32<<<grid_for(vec ? (n + 3) / 4 : n, 256), 256, 0, st>>>(dst, src, (long long)n, vec);
     return hipGetLastError();
 }
 

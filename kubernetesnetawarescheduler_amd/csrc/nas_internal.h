@@ -357,7 +357,7 @@ constexpr int32_t FLAG_TIMEOUT_HALT = 0x7ffffff0;
 hipError_t launch_flag_set(hipStream_t st, uint64_t *flag, uint64_t v);
 hipError_t launch_flag_wait(hipStream_t st, const uint64_t *flag, uint64_t v, int32_t *halt,
                             int64_t budget_ms);
-// dst[0, n) = src[0, n) (16-byte aligned buffers)
+// dst[0, n) = src[0, n) on st (16-byte moves when both are 16-byte aligned)
 hipError_t launch_copy_i32(hipStream_t st, int32_t *dst, const int32_t *src, int64_t n);
 hipError_t launch_pass_init(hipStream_t st, int32_t *status, const int32_t *cap, int32_t *cap_snap,
                             int n);
