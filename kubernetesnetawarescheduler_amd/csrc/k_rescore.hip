@@ -27,9 +27,12 @@ namespace {
 
 constexpr int STALE_THREADS = 256;
 // a pod is flagged when fewer than this many of its usable candidates still
-// fit: the dry ones (0) and those one commit away from running dry, whose
-// lists a herd of neighbours is about to drain
-constexpr int STALE_MIN_FIT = 2;
+// fit: the dry ones (0) and those a few commits away from running dry, whose
+// lists a herd of neighbours is about to drain.  4 (was 2): the full-range
+// herd's rescore rounds 27-56 -> 3-5 per pass and its pass 10.9 -> 9.7 ms
+// median on one box; 3, 6 and 8 within noise of 4, the pipelined passes
+// unchanged (profiles/r06w_ab_stale_min_fit.txt)
+constexpr int STALE_MIN_FIT = 4;
 
 // One launch: every block flags its pods (ballot words), and the LAST block
 // to finish (ticket counter ctl[3], zeroed at the start of every pass and
