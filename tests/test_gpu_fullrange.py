@@ -39,3 +39,26 @@ def test_profile_option_is_per_call(engine):
     engine.synth_cluster(SEED, 600, 512, "i8", peers=8, profile=0)
     _, L0, _, _ = engine.read_inputs(0, 0, want_L=True)
     assert L1.max() > 105 and L0.max() <= 105  # distance classes top out at 104
+
+
+def test_fullsize_fullrange_herd_passes_stay_few_rounds(engine):
+    """The full-size full-range herd (configs.C3_fullrange): after the pass
+    that discovers the herd, the herd plan with the cost-row cache and the
+    stale-scan threshold of 4 (k_rescore.hip STALE_MIN_FIT) needs only a few
+    rescore rounds per pass (27-56 with a threshold of 2), and every pass
+    places identically; the first pods equal the sequential oracle."""
+    N, P, sample = 10000, 100000, 512
+    engine.synth_cluster(SEED, N, P, "i8", peers=8, profile=1)
+    WA, L, cap, req = engine.read_inputs(0, sample, want_L=True)
+    runs = []
+    for _ in range(3):
+        engine.reset_capacity()
+        node, _, score = engine.place()
+        runs.append((node.copy(), score.copy(), engine.timings()["rescore_rounds"]))
+    first_rounds = runs[0][2]
+    assert first_rounds >= 8  # the discovery pass: pipelined plan, no cache
+    for node, score, rounds in runs[1:]:
+        assert (node == runs[0][0]).all() and (score == runs[0][1]).all()
+        assert rounds <= 16, rounds
+    want, wcost, _ = oracle.place(WA, L, req[:sample], cap, "i8")
+    assert (runs[0][0][:sample] == want).all() and (runs[0][1][:sample] == wcost).all()
